@@ -1,0 +1,359 @@
+// BLS12-381 base field Fp for gfx950: 14 limbs of 28 bits in 32-bit VGPRs,
+// Montgomery form with R = 2^392.
+//
+// Why radix 2^28: a 28x28-bit product is 56 bits, so a whole Montgomery
+// column (14 a*b products + 14 m*p products + carry) fits in one 64-bit
+// accumulator and every partial product is a single v_mad_u64_u32 with no
+// carry instructions (measured 64 G Fp-mul/s on MI355X vs 45 G for a 12x32
+// CIOS with addc chains, tools/microbench/fp_mul_bench.hip).
+//
+// Value-bound conventions (all limbs are always normalised to < 2^28, the
+// value is tracked in multiples of p):
+//   fp_mul / fp_sqr / fp_mul2   inputs < 32p (one may be < 64p), output < 2p
+//   fp_add                      output bound = sum of input bounds
+//   fp_sub(a, b)                a + 16p - b, requires b < 16p
+//   fp_reduce                   any value < 2^390 -> < 2p
+//   fp_canon                    -> canonical [0, p)
+// Define TBG_BOUNDS_CHECK in a host build to assert these at run time.
+#pragma once
+#include <cstdint>
+#include "bls_constants.h"
+
+#if defined(__HIP__)
+#define TBG_HD __host__ __device__ __forceinline__
+#else
+#define TBG_HD inline
+#endif
+
+#if defined(TBG_BOUNDS_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+#include <cstdio>
+#include <cstdlib>
+#define TBG_BOUND(cond, what) do { if (!(cond)) { fprintf(stderr, "bound violated: %s at %s:%d\n", what, __FILE__, __LINE__); abort(); } } while (0)
+#else
+#define TBG_BOUND(cond, what) do { } while (0)
+#endif
+
+namespace tbg {
+
+struct Fp { uint32_t l[NL]; };
+
+TBG_HD Fp fp_from_const(const uint32_t (&c)[NL]) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = c[i];
+  return r;
+}
+TBG_HD Fp fp_zero() {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = 0;
+  return r;
+}
+TBG_HD Fp fp_one() { return fp_from_const(ONE_M); }
+
+// Approximate value / p from the top limbs (host bound checks only).
+TBG_HD double fp_ratio_p(const Fp& a) {
+  double v = 0;
+  for (int i = NL - 1; i >= NL - 3; --i) v = v * 268435456.0 + (double)a.l[i];
+  double p = 0;
+  for (int i = NL - 1; i >= NL - 3; --i) p = p * 268435456.0 + (double)P_L[i];
+  return v / p;
+}
+
+TBG_HD void fp_normalize(Fp& a) {
+#pragma unroll
+  for (int i = 0; i < NL - 1; ++i) {
+    a.l[i + 1] += a.l[i] >> 28;
+    a.l[i] &= LMASK;
+  }
+}
+
+TBG_HD Fp fp_add(const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = a.l[i] + b.l[i];
+  fp_normalize(r);
+  return r;
+}
+
+TBG_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
+
+// a + 16p - b (b < 16p). SUB16P_L is 16p with every limb but the top one
+// >= 2^28 - 1, so no limb difference goes negative before normalisation.
+TBG_HD Fp fp_sub(const Fp& a, const Fp& b) {
+  TBG_BOUND(fp_ratio_p(b) <= 16.0, "fp_sub b <= 16p");
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = a.l[i] + SUB16P_L[i] - b.l[i];
+  fp_normalize(r);
+  return r;
+}
+
+TBG_HD Fp fp_neg(const Fp& a) {
+  TBG_BOUND(fp_ratio_p(a) <= 16.0, "fp_neg a <= 16p");
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = SUB16P_L[i] - a.l[i];
+  fp_normalize(r);
+  return r;
+}
+
+// a - q p for q = floor(a/p) or floor(a/p) - 1: result in [0, 2p).
+// Valid for a < 2^390.
+TBG_HD Fp fp_reduce(const Fp& a) {
+  TBG_BOUND(a.l[NL - 1] < (1u << 26), "fp_reduce a < 2^390");
+  // top 60 bits: a >> 330  (limb 13 holds bits 364.., limb 12 bits 336.., limb 11 bits 308..)
+  uint64_t t = ((uint64_t)a.l[13] << 34) | ((uint64_t)a.l[12] << 6) | (uint64_t)(a.l[11] >> 22);
+  double q = (double)t * INV_PT - 1e-9;
+  int32_t qi = q < 0.0 ? 0 : (int32_t)q;
+  Fp r;
+  int64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    int64_t s = (int64_t)a.l[i] + carry - (int64_t)qi * (int64_t)P_L[i];
+    r.l[i] = (uint32_t)s & LMASK;
+    carry = s >> 28;  // arithmetic shift
+  }
+  // the true result is in [0, 2p): the final carry is zero
+  return r;
+}
+
+// Conditional subtract of p: input < 2p -> [0, p).
+TBG_HD Fp fp_csub_p(const Fp& a) {
+  Fp d;
+  int32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    int32_t s = (int32_t)a.l[i] - (int32_t)P_L[i] + borrow;
+    d.l[i] = (uint32_t)s & LMASK;
+    borrow = s >> 28;
+  }
+  // borrow == -1 -> a < p, keep a
+  bool keep = borrow < 0;
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = keep ? a.l[i] : d.l[i];
+  return r;
+}
+
+TBG_HD Fp fp_canon(const Fp& a) { return fp_csub_p(fp_reduce(a)); }
+
+// Montgomery product REDC(sum_k a_k * b_k), product scanning, 28-bit limbs.
+// Column bound: 14 (K + 1) products of < 2^56 each, so K <= 16 fits 64 bits.
+template <int K>
+TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
+  uint32_t m[NL];
+  Fp r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; i <= k; ++i) {
+#pragma unroll
+      for (int n = 0; n < K; ++n) {
+        if (n & 1) s1 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
+        else s0 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < k; ++i) s2 += (uint64_t)m[i] * P_L[k - i];
+    uint64_t s = s0 + s1 + s2;
+    m[k] = ((uint32_t)s * NINV) & LMASK;
+    s += (uint64_t)m[k] * P_L[0];
+    acc = s >> 28;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; ++k) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; ++i) {
+#pragma unroll
+      for (int n = 0; n < K; ++n) {
+        if (n & 1) s1 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
+        else s0 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
+      }
+      s2 += (uint64_t)m[i] * P_L[k - i];
+    }
+    uint64_t s = s0 + s1 + s2;
+    r.l[k - NL] = (uint32_t)s & LMASK;
+    acc = s >> 28;
+  }
+  r.l[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+TBG_HD Fp fp_mul(const Fp& a, const Fp& b) {
+  TBG_BOUND(fp_ratio_p(a) * fp_ratio_p(b) < 2048.0, "fp_mul a*b < 2^11 p^2");
+  const Fp* const A[1] = {&a};
+  const Fp* const B[1] = {&b};
+  return fp_mul_sum<1>(A, B);
+}
+
+// REDC(a*b + c*d)
+TBG_HD Fp fp_mul2(const Fp& a, const Fp& b, const Fp& c, const Fp& d) {
+  TBG_BOUND(fp_ratio_p(a) * fp_ratio_p(b) + fp_ratio_p(c) * fp_ratio_p(d) < 2048.0, "fp_mul2 bound");
+  const Fp* const A[2] = {&a, &c};
+  const Fp* const B[2] = {&b, &d};
+  return fp_mul_sum<2>(A, B);
+}
+
+// Squaring: off-diagonal products once against a doubled copy.
+TBG_HD Fp fp_sqr(const Fp& a) {
+  TBG_BOUND(fp_ratio_p(a) * fp_ratio_p(a) < 2048.0, "fp_sqr bound");
+  uint32_t a2[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) a2[i] = a.l[i] << 1;
+  uint32_t m[NL];
+  Fp r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; 2 * i < k; ++i) {
+      if (i & 1) s1 += (uint64_t)a.l[i] * a2[k - i];
+      else s0 += (uint64_t)a.l[i] * a2[k - i];
+    }
+    if ((k & 1) == 0) s1 += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+    for (int i = 0; i < k; ++i) s2 += (uint64_t)m[i] * P_L[k - i];
+    uint64_t s = s0 + s1 + s2;
+    m[k] = ((uint32_t)s * NINV) & LMASK;
+    s += (uint64_t)m[k] * P_L[0];
+    acc = s >> 28;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; ++k) {
+    uint64_t s0 = acc, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int i = k - NL + 1; 2 * i < k; ++i) {
+      if (i & 1) s1 += (uint64_t)a.l[i] * a2[k - i];
+      else s0 += (uint64_t)a.l[i] * a2[k - i];
+    }
+    if ((k & 1) == 0) s1 += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; ++i) s2 += (uint64_t)m[i] * P_L[k - i];
+    uint64_t s = s0 + s1 + s2;
+    r.l[k - NL] = (uint32_t)s & LMASK;
+    acc = s >> 28;
+  }
+  r.l[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// a * k for a small constant k (k * 2^28 * 16 fits): normalised, no reduction.
+TBG_HD Fp fp_mul_small(const Fp& a, uint32_t k) {
+  Fp r;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; ++i) {
+    uint64_t s = (uint64_t)a.l[i] * k + carry;
+    r.l[i] = (uint32_t)s & LMASK;
+    carry = s >> 28;
+  }
+  r.l[NL - 1] = (uint32_t)((uint64_t)a.l[NL - 1] * k + carry);
+  return r;
+}
+
+TBG_HD bool fp_is_zero(const Fp& a) {
+  Fp c = fp_canon(a);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) o |= c.l[i];
+  return o == 0;
+}
+
+TBG_HD bool fp_eq(const Fp& a, const Fp& b) {
+  Fp ca = fp_canon(a), cb = fp_canon(b);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) o |= ca.l[i] ^ cb.l[i];
+  return o == 0;
+}
+
+TBG_HD Fp fp_select(bool c, const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+
+// Montgomery -> canonical integer limbs.
+TBG_HD Fp fp_from_mont(const Fp& a) {
+  Fp one = fp_zero();
+  one.l[0] = 1;
+  return fp_canon(fp_mul(a, one));
+}
+
+// Canonical integer limbs (< 2^384) -> Montgomery form.
+TBG_HD Fp fp_to_mont(const Fp& a) {
+  Fp r2 = fp_from_const(R2_M);
+  return fp_mul(a, r2);
+}
+
+// Exponentiation by a fixed public exponent (square and multiply, MSB first).
+template <int NBITS, int NW>
+TBG_HD Fp fp_pow_const(const Fp& a, const uint32_t (&w)[NW]) {
+  Fp r = a;  // top bit is 1
+  for (int i = NBITS - 2; i >= 0; --i) {
+    r = fp_sqr(r);
+    if ((w[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+TBG_HD Fp fp_inv(const Fp& a) { return fp_pow_const<EXP_INV_BITS>(a, EXP_INV_WORDS); }
+
+// Big-endian bytes (48) -> integer limbs; also reports whether value < p.
+TBG_HD Fp fp_limbs_from_be48(const uint8_t* b, bool* lt_p) {
+  Fp r = fp_zero();
+  // bit position of byte j (from the end): 8 * (47 - j)
+#pragma unroll
+  for (int j = 0; j < 48; ++j) {
+    int bit = 8 * (47 - j);
+    uint32_t v = b[j];
+    int li = bit / 28, off = bit % 28;
+    r.l[li] |= (v << off) & LMASK;
+    if (off > 20 && li + 1 < NL) r.l[li + 1] |= v >> (28 - off);
+  }
+  if (lt_p) {
+    int32_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      int32_t s = (int32_t)r.l[i] - (int32_t)P_L[i] + borrow;
+      borrow = s >> 28;
+    }
+    *lt_p = borrow < 0;
+  }
+  return r;
+}
+
+// Canonical integer limbs -> 48 big-endian bytes.
+TBG_HD void fp_limbs_to_be48(const Fp& a, uint8_t* b) {
+#pragma unroll
+  for (int j = 0; j < 48; ++j) {
+    int bit = 8 * (47 - j);
+    int li = bit / 28, off = bit % 28;
+    uint32_t v = a.l[li] >> off;
+    if (off > 20 && li + 1 < NL) v |= a.l[li + 1] << (28 - off);
+    b[j] = (uint8_t)v;
+  }
+}
+
+// lexicographically largest (ZCash): canonical value > (p-1)/2
+TBG_HD bool fp_lex_largest_canon(const Fp& c) {
+  // compare 2c > p - 1  <=>  2c >= p  (c < p)
+  Fp d = fp_add(c, c);
+  int32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    int32_t s = (int32_t)d.l[i] - (int32_t)P_L[i] + borrow;
+    borrow = s >> 28;
+  }
+  return borrow == 0;
+}
+
+TBG_HD uint32_t fp_parity_canon(const Fp& c) { return c.l[0] & 1; }
+
+}  // namespace tbg

@@ -1,0 +1,203 @@
+// hash_to_curve for G2 (RFC 9380 suite BLS12381G2_XMD:SHA-256_SSWU_RO_) with
+// the proof-of-possession DST used by kryptology's SigEth2 (reference
+// tbls/tss.go:28-31): expand_message_xmd(SHA-256) -> hash_to_field (Fp2, 2
+// elements) -> simplified SWU on E2' -> 3-isogeny -> sum -> cofactor clearing.
+#pragma once
+#include "bls_curve.h"
+
+namespace tbg {
+
+// ------------------------------------------------------------------ SHA-256
+struct Sha256 {
+  uint32_t h[8];
+  uint8_t buf[64];
+  uint32_t nbuf;
+  uint64_t total;
+};
+
+TBG_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+TBG_HD void sha256_init(Sha256& s) {
+  const uint32_t iv[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                          0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  for (int i = 0; i < 8; ++i) s.h[i] = iv[i];
+  s.nbuf = 0;
+  s.total = 0;
+}
+
+TBG_HD void sha256_block(uint32_t (&h)[8], const uint8_t* blk) {
+  const uint32_t K[64] = {
+      0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+      0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+      0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+      0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+      0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+      0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+      0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+      0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+  uint32_t w[64];
+  for (int i = 0; i < 16; ++i)
+    w[i] = ((uint32_t)blk[4 * i] << 24) | ((uint32_t)blk[4 * i + 1] << 16) | ((uint32_t)blk[4 * i + 2] << 8) | blk[4 * i + 3];
+  for (int i = 16; i < 64; ++i) {
+    uint32_t s0 = rotr32(w[i - 15], 7) ^ rotr32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = rotr32(w[i - 2], 17) ^ rotr32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 64; ++i) {
+    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = hh + S1 + ch + K[i] + w[i];
+    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+TBG_HD void sha256_byte(Sha256& s, uint8_t v) {
+  s.buf[s.nbuf++] = v;
+  s.total++;
+  if (s.nbuf == 64) {
+    sha256_block(s.h, s.buf);
+    s.nbuf = 0;
+  }
+}
+
+TBG_HD void sha256_update(Sha256& s, const uint8_t* p, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) sha256_byte(s, p[i]);
+}
+
+TBG_HD void sha256_final(Sha256& s, uint8_t* out) {
+  uint64_t bits = s.total * 8;
+  sha256_byte(s, 0x80);
+  while (s.nbuf != 56) sha256_byte(s, 0);
+  for (int i = 7; i >= 0; --i) sha256_byte(s, (uint8_t)(bits >> (8 * i)));
+  for (int i = 0; i < 8; ++i) {
+    out[4 * i] = (uint8_t)(s.h[i] >> 24);
+    out[4 * i + 1] = (uint8_t)(s.h[i] >> 16);
+    out[4 * i + 2] = (uint8_t)(s.h[i] >> 8);
+    out[4 * i + 3] = (uint8_t)s.h[i];
+  }
+}
+
+// DST = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_" (43 bytes)
+constexpr int DST_LEN = 43;
+TBG_HD uint8_t dst_byte(int i) {
+  const char d[DST_LEN + 1] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_";
+  return (uint8_t)d[i];
+}
+TBG_HD void sha256_dst_prime(Sha256& s) {
+  for (int i = 0; i < DST_LEN; ++i) sha256_byte(s, dst_byte(i));
+  sha256_byte(s, (uint8_t)DST_LEN);
+}
+
+// expand_message_xmd(msg, DST, 256): out[256]
+TBG_HD void expand_message_xmd_256(const uint8_t* msg, uint32_t msg_len, uint8_t* out) {
+  Sha256 s;
+  sha256_init(s);
+  for (int i = 0; i < 64; ++i) sha256_byte(s, 0);
+  sha256_update(s, msg, msg_len);
+  sha256_byte(s, 0x01);  // l_i_b_str = I2OSP(256, 2)
+  sha256_byte(s, 0x00);
+  sha256_byte(s, 0x00);  // I2OSP(0, 1)
+  sha256_dst_prime(s);
+  uint8_t b0[32];
+  sha256_final(s, b0);
+  uint8_t bi[32];
+  for (int i = 1; i <= 8; ++i) {
+    sha256_init(s);
+    if (i == 1) {
+      sha256_update(s, b0, 32);
+    } else {
+      for (int j = 0; j < 32; ++j) sha256_byte(s, b0[j] ^ bi[j]);
+    }
+    sha256_byte(s, (uint8_t)i);
+    sha256_dst_prime(s);
+    sha256_final(s, bi);
+    for (int j = 0; j < 32; ++j) out[32 * (i - 1) + j] = bi[j];
+  }
+}
+
+// 32 big-endian bytes -> 14 limbs (value < 2^256)
+TBG_HD Fp limbs_from_be32(const uint8_t* b) {
+  Fp r = fp_zero();
+  for (int j = 0; j < 32; ++j) {
+    int bit = 8 * (31 - j);
+    uint32_t v = b[j];
+    int li = bit / 28, off = bit % 28;
+    r.l[li] |= (v << off) & LMASK;
+    if (off > 20) r.l[li + 1] |= v >> (28 - off);
+  }
+  return r;
+}
+
+// 64 big-endian bytes mod p, in Montgomery form: REDC(hi * 2^256 R^2 + lo * R^2)
+TBG_HD Fp fp_from_be64_mod(const uint8_t* b) {
+  Fp hi = limbs_from_be32(b), lo = limbs_from_be32(b + 32);
+  Fp ca = fp_from_const(R2_2E256_M), cb = fp_from_const(R2_M);
+  return fp_mul2(hi, ca, lo, cb);
+}
+
+TBG_HD void hash_to_field_fp2(const uint8_t* msg, uint32_t msg_len, Fp2& u0, Fp2& u1) {
+  uint8_t uni[256];
+  expand_message_xmd_256(msg, msg_len, uni);
+  u0.c0 = fp_from_be64_mod(uni);
+  u0.c1 = fp_from_be64_mod(uni + 64);
+  u1.c0 = fp_from_be64_mod(uni + 128);
+  u1.c1 = fp_from_be64_mod(uni + 192);
+}
+
+// Simplified SWU to E2' then the 3-isogeny to E2, output Jacobian on E2.
+TBG_HD G2J map_to_curve_g2(const Fp2& u) {
+  Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B), Z = fp2_from_const(SSWU_Z);
+  Fp2 u2 = fp2_sqr(u);
+  Fp2 zu2 = fp2_mul(Z, u2);
+  Fp2 den = fp2_reduce(fp2_add(fp2_sqr(zu2), zu2));
+  Fp2 x1;
+  if (fp2_is_zero(den)) {
+    x1 = fp2_from_const(SSWU_B_OVER_ZA);
+  } else {
+    Fp2 t = fp2_reduce(fp2_add(fp2_one(), fp2_inv(den)));
+    x1 = fp2_mul(fp2_from_const(SSWU_NEG_B_OVER_A), t);
+  }
+  Fp2 gx1 = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_sqr(x1), x1), fp2_mul(A, x1)), B));
+  Fp2 x, y;
+  if (fp2_sqrt(gx1, y)) {
+    x = x1;
+  } else {
+    x = fp2_mul(zu2, x1);
+    Fp2 gx2 = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_sqr(x), x), fp2_mul(A, x)), B));
+    fp2_sqrt(gx2, y);  // always a square when gx1 is not
+  }
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_reduce(fp2_neg(y));
+  // 3-isogeny: x = x_num / x_den, y = y' y_num / y_den, as Jacobian
+  // (X, Y, Z) = (x_num x_den y_den^2, y' y_num x_den^3 y_den^2, x_den y_den).
+  Fp2 xx = fp2_sqr(x), xxx = fp2_mul(xx, x);
+  Fp2 xnum = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_from_const(ISO_K13), xxx), fp2_mul(fp2_from_const(ISO_K12), xx)),
+                                fp2_add(fp2_mul(fp2_from_const(ISO_K11), x), fp2_from_const(ISO_K10))));
+  Fp2 xden = fp2_reduce(fp2_add(fp2_add(xx, fp2_mul(fp2_from_const(ISO_K21), x)), fp2_from_const(ISO_K20)));
+  Fp2 ynum = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_from_const(ISO_K33), xxx), fp2_mul(fp2_from_const(ISO_K32), xx)),
+                                fp2_add(fp2_mul(fp2_from_const(ISO_K31), x), fp2_from_const(ISO_K30))));
+  Fp2 yden = fp2_reduce(fp2_add(fp2_add(xxx, fp2_mul(fp2_from_const(ISO_K42), xx)),
+                                fp2_add(fp2_mul(fp2_from_const(ISO_K41), x), fp2_from_const(ISO_K40))));
+  Fp2 yden2 = fp2_sqr(yden);
+  G2J r;
+  r.Z = fp2_mul(xden, yden);
+  r.X = fp2_mul(fp2_mul(xnum, xden), yden2);
+  Fp2 xden3 = fp2_mul(fp2_sqr(xden), xden);
+  r.Y = fp2_mul(fp2_mul(fp2_mul(y, ynum), xden3), yden2);
+  return r;
+}
+
+// H(m) in G2 (Jacobian).
+TBG_HD G2J hash_to_g2(const uint8_t* msg, uint32_t msg_len) {
+  Fp2 u0, u1;
+  hash_to_field_fp2(msg, msg_len, u0, u1);
+  G2J q0 = map_to_curve_g2(u0);
+  G2J q1 = map_to_curve_g2(u1);
+  return g2_clear_cofactor(jac_add(q0, q1));
+}
+
+}  // namespace tbg

@@ -1,0 +1,245 @@
+// Extension tower for BLS12-381 on gfx950:
+//   Fp2  = Fp[u]  / (u^2 + 1)
+//   Fp6  = Fp2[v] / (v^3 - xi),  xi = 1 + u
+//   Fp12 = Fp6[w] / (w^2 - v)
+//
+// Bound conventions (multiples of p per Fp component; see bls_field.h):
+//   fp2_mul / fp2_sqr      inputs < 16p, output < 2p
+//   fp6_mul / fp6_sqr      inputs <  8p, output < 2p
+//   fp12_mul / fp12_sqr    inputs <  4p, output < 2p
+//   *_add / *_sub / *_neg  lazy (no reduction), the caller tracks growth
+//   *_reduce               -> < 2p
+#pragma once
+#include "bls_field.h"
+
+namespace tbg {
+
+struct Fp2 { Fp c0, c1; };
+struct Fp6 { Fp2 c0, c1, c2; };
+struct Fp12 { Fp6 c0, c1; };
+
+// ----------------------------------------------------------------- Fp2
+TBG_HD Fp2 fp2_from_const(const Fp2Const& c) { return {fp_from_const(c.c0), fp_from_const(c.c1)}; }
+TBG_HD Fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
+TBG_HD Fp2 fp2_one() { return {fp_one(), fp_zero()}; }
+TBG_HD Fp2 fp2_add(const Fp2& a, const Fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+TBG_HD Fp2 fp2_dbl(const Fp2& a) { return fp2_add(a, a); }
+TBG_HD Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+TBG_HD Fp2 fp2_neg(const Fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+TBG_HD Fp2 fp2_conj(const Fp2& a) { return {a.c0, fp_neg(a.c1)}; }
+TBG_HD Fp2 fp2_reduce(const Fp2& a) { return {fp_reduce(a.c0), fp_reduce(a.c1)}; }
+TBG_HD Fp2 fp2_canon(const Fp2& a) { return {fp_canon(a.c0), fp_canon(a.c1)}; }
+TBG_HD Fp2 fp2_select(bool c, const Fp2& a, const Fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
+TBG_HD Fp2 fp2_mul_small(const Fp2& a, uint32_t k) { return {fp_mul_small(a.c0, k), fp_mul_small(a.c1, k)}; }
+
+TBG_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+  Fp nb1 = fp_neg(b.c1);
+  return {fp_mul2(a.c0, b.c0, a.c1, nb1), fp_mul2(a.c0, b.c1, a.c1, b.c0)};
+}
+
+TBG_HD Fp2 fp2_sqr(const Fp2& a) {
+  Fp s = fp_add(a.c0, a.c1);
+  Fp d = fp_sub(a.c0, a.c1);
+  Fp a0d = fp_dbl(a.c0);
+  return {fp_mul(s, d), fp_mul(a0d, a.c1)};
+}
+
+TBG_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return {fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
+
+// (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u   [lazy: c0 < a0 + 16p, c1 < a0 + a1]
+TBG_HD Fp2 fp2_mul_xi(const Fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+TBG_HD bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+TBG_HD bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+
+TBG_HD Fp2 fp2_inv(const Fp2& a) {
+  Fp n = fp_mul2(a.c0, a.c0, a.c1, a.c1);
+  Fp t = fp_inv(n);
+  return {fp_mul(a.c0, t), fp_mul(fp_neg(a.c1), t)};
+}
+
+// Square root in Fp2 via two Fp exponentiations (norm method).
+// Returns false when a is not a square.  The root returned is unspecified
+// up to sign; callers fix the sign.
+TBG_HD bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
+  Fp2 a = fp2_reduce(a_in);
+  bool a1_zero = fp_is_zero(a.c1);
+  if (a1_zero) {
+    // a in Fp: sqrt(a0) or u * sqrt(-a0)
+    Fp s = fp_pow_const<EXP_SQRT_BITS>(a.c0, EXP_SQRT_WORDS);
+    if (fp_eq(fp_sqr(s), a.c0)) { out = {s, fp_zero()}; return true; }
+    Fp na = fp_neg(a.c0);
+    Fp s2 = fp_pow_const<EXP_SQRT_BITS>(na, EXP_SQRT_WORDS);
+    if (fp_eq(fp_sqr(s2), na)) { out = {fp_zero(), s2}; return true; }
+    return false;
+  }
+  Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
+  Fp gamma = fp_pow_const<EXP_SQRT_BITS>(norm, EXP_SQRT_WORDS);
+  if (!fp_eq(fp_sqr(gamma), norm)) return false;
+  Fp inv2 = fp_from_const(INV2_M);
+  Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);  // non-zero because a1 != 0
+  Fp t = fp_pow_const<EXP_PM3D4_BITS>(delta, EXP_PM3D4_WORDS);  // delta^((p-3)/4)
+  Fp x0 = fp_mul(delta, t);
+  Fp x0sq = fp_sqr(x0);
+  Fp2 r;
+  if (fp_eq(x0sq, delta)) {
+    // delta is a residue: x0 = sqrt(delta), x1 = a1 / (2 x0) = a1 t / 2
+    r.c0 = x0;
+    r.c1 = fp_mul(fp_mul(a.c1, t), inv2);
+  } else {
+    // non-residue: x0 = a1 t / 2, x1 = -delta t
+    r.c0 = fp_mul(fp_mul(a.c1, t), inv2);
+    r.c1 = fp_neg(x0);
+  }
+  if (!fp2_eq(fp2_sqr(r), a)) return false;
+  out = r;
+  return true;
+}
+
+// Legendre-style square test in Fp2: a is a square iff norm(a) is a square in Fp.
+TBG_HD bool fp2_is_square(const Fp2& a) {
+  Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
+  if (fp_is_zero(norm)) return true;
+  Fp l = fp_pow_const<EXP_LEGENDRE_BITS>(norm, EXP_LEGENDRE_WORDS);
+  return fp_eq(l, fp_one());
+}
+
+// RFC 9380 sgn0 for Fp2 (on canonical values)
+TBG_HD uint32_t fp2_sgn0(const Fp2& a) {
+  Fp c0 = fp_from_mont(a.c0), c1 = fp_from_mont(a.c1);
+  uint32_t s0 = c0.l[0] & 1;
+  uint32_t z0 = 1;
+  for (int i = 0; i < NL; ++i) z0 &= (c0.l[i] == 0);
+  uint32_t s1 = c1.l[0] & 1;
+  return s0 | (z0 & s1);
+}
+
+// ZCash: lexicographically largest, c1 first then c0 (Montgomery input)
+TBG_HD bool fp2_lex_largest(const Fp2& a) {
+  Fp c0 = fp_from_mont(a.c0), c1 = fp_from_mont(a.c1);
+  uint32_t z1 = 0;
+  for (int i = 0; i < NL; ++i) z1 |= c1.l[i];
+  if (z1 != 0) return fp_lex_largest_canon(c1);
+  return fp_lex_largest_canon(c0);
+}
+
+// ----------------------------------------------------------------- Fp6
+TBG_HD Fp6 fp6_zero() { return {fp2_zero(), fp2_zero(), fp2_zero()}; }
+TBG_HD Fp6 fp6_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
+TBG_HD Fp6 fp6_add(const Fp6& a, const Fp6& b) { return {fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+TBG_HD Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return {fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+TBG_HD Fp6 fp6_neg(const Fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+TBG_HD Fp6 fp6_reduce(const Fp6& a) { return {fp2_reduce(a.c0), fp2_reduce(a.c1), fp2_reduce(a.c2)}; }
+// (a0 + a1 v + a2 v^2) v = xi a2 + a0 v + a1 v^2  (lazy)
+TBG_HD Fp6 fp6_mul_v(const Fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+// Karatsuba (6 Fp2 products). Inputs < 8p, output < 2p.
+TBG_HD Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+  Fp2 t0 = fp2_mul(a.c0, b.c0);
+  Fp2 t1 = fp2_mul(a.c1, b.c1);
+  Fp2 t2 = fp2_mul(a.c2, b.c2);
+  Fp2 s12 = fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2));
+  Fp2 s01 = fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1));
+  Fp2 s02 = fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2));
+  Fp2 u = fp2_reduce(fp2_sub(s12, fp2_add(t1, t2)));         // < 2p
+  Fp2 c0 = fp2_reduce(fp2_add(t0, fp2_mul_xi(u)));             // t0 + xi(s12 - t1 - t2)
+  Fp2 c1 = fp2_reduce(fp2_add(fp2_sub(s01, fp2_add(t0, t1)), fp2_mul_xi(t2)));
+  Fp2 c2 = fp2_reduce(fp2_add(fp2_sub(s02, fp2_add(t0, t2)), t1));
+  return {c0, c1, c2};
+}
+
+TBG_HD Fp6 fp6_sqr(const Fp6& a) { return fp6_mul(a, a); }
+
+// a * (b0 + b1 v): 5 Fp2 products.  Inputs < 8p, output < 2p.
+TBG_HD Fp6 fp6_mul_by_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
+  Fp2 t0 = fp2_mul(a.c0, b0);
+  Fp2 t1 = fp2_mul(a.c1, b1);
+  Fp2 s01 = fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1));
+  Fp2 a2b1 = fp2_mul(a.c2, b1);
+  Fp2 a2b0 = fp2_mul(a.c2, b0);
+  Fp2 c0 = fp2_reduce(fp2_add(t0, fp2_mul_xi(a2b1)));
+  Fp2 c1 = fp2_reduce(fp2_sub(s01, fp2_add(t0, t1)));
+  Fp2 c2 = fp2_reduce(fp2_add(t1, a2b0));
+  return {c0, c1, c2};
+}
+
+// a * (b1 v): 3 Fp2 products.
+TBG_HD Fp6 fp6_mul_by_1(const Fp6& a, const Fp2& b1) {
+  Fp2 t0 = fp2_mul(a.c2, b1);
+  Fp2 t1 = fp2_mul(a.c0, b1);
+  Fp2 t2 = fp2_mul(a.c1, b1);
+  return {fp2_reduce(fp2_mul_xi(t0)), t1, t2};
+}
+
+TBG_HD Fp6 fp6_inv(const Fp6& a) {
+  Fp2 c0 = fp2_reduce(fp2_sub(fp2_sqr(a.c0), fp2_reduce(fp2_mul_xi(fp2_mul(a.c1, a.c2)))));
+  Fp2 c1 = fp2_reduce(fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1)));
+  Fp2 c2 = fp2_reduce(fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2)));
+  Fp2 t = fp2_reduce(fp2_add(fp2_mul(a.c0, c0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, c1), fp2_mul(a.c1, c2)))));
+  Fp2 ti = fp2_inv(t);
+  return {fp2_mul(c0, ti), fp2_mul(c1, ti), fp2_mul(c2, ti)};
+}
+
+// ----------------------------------------------------------------- Fp12
+TBG_HD Fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
+TBG_HD Fp12 fp12_conj(const Fp12& a) { return {a.c0, fp6_reduce(fp6_neg(a.c1))}; }
+
+// Inputs < 4p, output < 2p.
+TBG_HD Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
+  Fp6 t0 = fp6_mul(a.c0, b.c0);
+  Fp6 t1 = fp6_mul(a.c1, b.c1);
+  Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1));
+  Fp6 c1 = fp6_reduce(fp6_sub(s, fp6_add(t0, t1)));
+  Fp6 c0 = fp6_reduce(fp6_add(t0, fp6_mul_v(t1)));
+  return {c0, c1};
+}
+
+// Complex squaring: 2 Fp6 products.
+TBG_HD Fp12 fp12_sqr(const Fp12& a) {
+  Fp6 t = fp6_mul(a.c0, a.c1);                                   // < 2p
+  Fp6 va1 = fp6_reduce(fp6_mul_v(a.c1));
+  Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, va1));      // (a0+a1)(a0+v a1)
+  Fp6 tvt = fp6_reduce(fp6_add(t, fp6_mul_v(t)));
+  Fp6 c0 = fp6_reduce(fp6_sub(s, tvt));
+  Fp6 c1 = fp6_reduce(fp6_add(t, t));
+  return {c0, c1};
+}
+
+// f * (l0 + l1 v + l4 v w): the Miller-loop line (positions 0, 1, 4).
+TBG_HD Fp12 fp12_mul_by_014(const Fp12& a, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
+  Fp6 t0 = fp6_mul_by_01(a.c0, l0, l1);
+  Fp6 t1 = fp6_mul_by_1(a.c1, l4);
+  Fp6 s = fp6_mul_by_01(fp6_add(a.c0, a.c1), l0, fp2_add(l1, l4));
+  Fp6 c1 = fp6_reduce(fp6_sub(s, fp6_add(t0, t1)));
+  Fp6 c0 = fp6_reduce(fp6_add(t0, fp6_mul_v(t1)));
+  return {c0, c1};
+}
+
+TBG_HD Fp12 fp12_inv(const Fp12& a) {
+  Fp6 t = fp6_reduce(fp6_sub(fp6_mul(a.c0, a.c0), fp6_reduce(fp6_mul_v(fp6_mul(a.c1, a.c1)))));
+  Fp6 ti = fp6_inv(t);
+  return {fp6_mul(a.c0, ti), fp6_reduce(fp6_neg(fp6_mul(a.c1, ti)))};
+}
+
+// f^p: conj every Fp2 coefficient and multiply by gamma_k = xi^(k(p-1)/6),
+// with f = sum a_k w^k, a_0 = c0.c0, a_1 = c1.c0, a_2 = c0.c1, a_3 = c1.c1,
+// a_4 = c0.c2, a_5 = c1.c2.
+TBG_HD Fp12 fp12_frob(const Fp12& a) {
+  Fp12 r;
+  r.c0.c0 = fp2_reduce(fp2_conj(a.c0.c0));
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), fp2_from_const(FROB_G2));
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), fp2_from_const(FROB_G4));
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), fp2_from_const(FROB_G1));
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), fp2_from_const(FROB_G3));
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), fp2_from_const(FROB_G5));
+  return r;
+}
+
+TBG_HD bool fp12_is_one(const Fp12& a) {
+  bool ok = fp_eq(a.c0.c0.c0, fp_one()) && fp_is_zero(a.c0.c0.c1);
+  ok = ok && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2);
+  ok = ok && fp2_is_zero(a.c1.c0) && fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
+  return ok;
+}
+
+}  // namespace tbg

@@ -1,0 +1,190 @@
+"""The engine's device arithmetic, compiled for the host, against the oracle.
+
+The HIP kernels include exactly these headers (charon_amd/csrc/bls_*.h); the
+host build runs with TBG_BOUNDS_CHECK so a violated lazy-reduction bound
+aborts the test process.  GPU parity is covered separately (-m gpu)."""
+import random
+
+import pytest
+
+from oracle import bls12_381 as bls
+from oracle import tbls_oracle as tb
+from tests.hostcheck import lib
+
+P = bls.P
+rng = random.Random(20241015)
+
+
+def be(x):
+    return x.to_bytes(48, "big")
+
+
+def fe(b):
+    return int.from_bytes(b, "big")
+
+
+def call(fn, *args, out=48):
+    buf = (bytes(out))
+    import ctypes
+    ob = ctypes.create_string_buffer(out)
+    getattr(lib(), fn)(*args, ob)
+    return ob.raw
+
+
+EDGE = [0, 1, 2, P - 1, P - 2, (P - 1) // 2, (1 << 380) % P, (1 << 381) - 1 - P]
+
+
+def samples(n=40):
+    return EDGE + [rng.randrange(P) for _ in range(n)]
+
+
+def test_fp_ops():
+    vals = samples()
+    for a in vals:
+        for b in vals[:12] + [rng.randrange(P)]:
+            assert fe(call("hc_fp_mul", be(a), be(b))) == a * b % P
+            assert fe(call("hc_fp_add", be(a), be(b))) == (a + b) % P
+            assert fe(call("hc_fp_sub", be(a), be(b))) == (a - b) % P
+        assert fe(call("hc_fp_sqr", be(a))) == a * a % P
+    for a in vals[1:10]:
+        if a % P:
+            assert fe(call("hc_fp_inv", be(a))) == pow(a, P - 2, P)
+
+
+def f2b(x):
+    return be(x[0]) + be(x[1])
+
+
+def b2f(b):
+    return (fe(b[:48]), fe(b[48:96]))
+
+
+def test_fp2_mul_and_sqrt():
+    for _ in range(30):
+        a = (rng.randrange(P), rng.randrange(P))
+        b = (rng.randrange(P), rng.randrange(P))
+        assert b2f(call("hc_fp2_mul", f2b(a), f2b(b), out=96)) == bls.f2_mul(a, b)
+        sq = bls.f2_sqr(a)
+        import ctypes
+        ob = ctypes.create_string_buffer(96)
+        assert lib().hc_fp2_sqrt(f2b(sq), ob) == 1
+        r = b2f(ob.raw)
+        assert bls.f2_sqr(r) == sq
+    # non-squares and the a1 == 0 branch
+    for _ in range(10):
+        a = (rng.randrange(P), rng.randrange(P))
+        import ctypes
+        ob = ctypes.create_string_buffer(96)
+        ok = lib().hc_fp2_sqrt(f2b(a), ob)
+        assert ok == (1 if bls.f2_is_square(a) else 0)
+        if ok:
+            assert bls.f2_sqr(b2f(ob.raw)) == a
+    for a0 in [0, 1, 2, 3, P - 1, rng.randrange(P)]:
+        import ctypes
+        ob = ctypes.create_string_buffer(96)
+        ok = lib().hc_fp2_sqrt(f2b((a0, 0)), ob)
+        assert ok == 1  # every Fp element is a square in Fp2
+        assert bls.f2_sqr(b2f(ob.raw)) == (a0, 0)
+
+
+def f12b(f):
+    (a, b, c), (d, e, g) = f
+    return b"".join(f2b(x) for x in (a, b, c, d, e, g))
+
+
+def b2f12(bb):
+    xs = [b2f(bb[96 * i:96 * i + 96]) for i in range(6)]
+    return ((xs[0], xs[1], xs[2]), (xs[3], xs[4], xs[5]))
+
+
+def rand_f12():
+    return tuple(tuple((rng.randrange(P), rng.randrange(P)) for _ in range(3)) for _ in range(2))
+
+
+def test_fp12_ops():
+    for _ in range(6):
+        a, b = rand_f12(), rand_f12()
+        assert b2f12(call("hc_fp12_mul", f12b(a), f12b(b), out=576)) == bls.f12_mul(a, b)
+        assert b2f12(call("hc_fp12_sqr", f12b(a), out=576)) == bls.f12_sqr(a)
+        assert b2f12(call("hc_fp12_inv", f12b(a), out=576)) == bls.f12_inv(a)
+        assert b2f12(call("hc_fp12_frob", f12b(a), out=576)) == bls.f12_frob(a)
+
+
+def test_final_exp_matches_oracle():
+    a = rand_f12()
+    assert b2f12(call("hc_final_exp", f12b(a), out=576)) == bls.final_exp(a)
+
+
+def aff2b(q):
+    return f2b(q[0]) + f2b(q[1])
+
+
+def test_miller_loop_after_final_exp():
+    p = bls.g1_mul(bls.G1_GEN, rng.randrange(1, bls.R))
+    q = bls.g2_mul(bls.G2_GEN, rng.randrange(1, bls.R))
+    m = b2f12(call("hc_miller", be(p[0]) + be(p[1]), aff2b(q), out=576))
+    # the device scales its lines by Fp2 factors; only the final-exponentiated values must agree
+    assert bls.final_exp(m) == bls.pairing(p, q)
+
+
+def test_g2_decompress_matches_oracle():
+    import ctypes
+    for _ in range(6):
+        q = bls.g2_mul(bls.G2_GEN, rng.randrange(1, bls.R))
+        enc = bls.g2_compress(q)
+        ob = ctypes.create_string_buffer(192)
+        assert lib().hc_g2_decompress(enc, ob) == 0
+        assert (b2f(ob.raw[:96]), b2f(ob.raw[96:])) == q
+    # error classes
+    ob = ctypes.create_string_buffer(192)
+    assert lib().hc_g2_decompress(bytes([0xC0]) + bytes(95), ob) == 1          # identity
+    assert lib().hc_g2_decompress(bytes(96), ob) == -1                         # no compression flag
+    assert lib().hc_g2_decompress(bytes([0x9F]) + b"\xff" * 95, ob) == -2      # x >= p
+
+
+def test_g2_decompress_rejects_off_curve_and_non_subgroup():
+    import ctypes
+    n_off = n_sub = 0
+    for _ in range(12):
+        x = (rng.randrange(P), rng.randrange(P))
+        y2 = bls.f2_add(bls.f2_mul(bls.f2_sqr(x), x), bls.B2)
+        enc = bytearray(x[1].to_bytes(48, "big") + x[0].to_bytes(48, "big"))
+        enc[0] |= 0x80
+        ob = ctypes.create_string_buffer(192)
+        st = lib().hc_g2_decompress(bytes(enc), ob)
+        if bls.f2_sqrt(y2) is None:
+            assert st == -3
+            n_off += 1
+        else:
+            assert st == -4  # random curve points are outside G2 (cofactor h2 is huge)
+            n_sub += 1
+    assert n_off and n_sub
+
+
+def test_hash_to_g2_matches_oracle():
+    for msg in [b"", b"abc", bytes(32), bytes(range(32)), b"Hello Obol", bytes(range(200))]:
+        h = call("hc_hash_to_g2", msg, len(msg), out=96)
+        assert h == bls.g2_compress(bls.hash_to_g2(msg))
+
+
+def test_core_verify_kat_and_rejects():
+    from tests.test_oracle_kat import DEPOSIT_GOLDEN, deposit_signing_root
+    for pk_hex, sig_hex, root_hex in DEPOSIT_GOLDEN[:2]:
+        pk, sig, root = bytes.fromhex(pk_hex), bytes.fromhex(sig_hex), deposit_signing_root(root_hex)
+        assert lib().hc_verify(pk, root, len(root), sig) == 1
+        bad = bytearray(root)
+        bad[0] ^= 1
+        assert lib().hc_verify(pk, bytes(bad), len(bad), sig) == 0
+    # wrong key
+    pk2 = bytes.fromhex(DEPOSIT_GOLDEN[2][0])
+    pk, sig, root = bytes.fromhex(DEPOSIT_GOLDEN[0][0]), bytes.fromhex(DEPOSIT_GOLDEN[0][1]), deposit_signing_root(DEPOSIT_GOLDEN[0][2])
+    assert lib().hc_verify(pk2, root, len(root), sig) == 0
+
+
+def test_g1_decompress_matches_oracle():
+    import ctypes
+    for _ in range(4):
+        p = bls.g1_mul(bls.G1_GEN, rng.randrange(1, bls.R))
+        ob = ctypes.create_string_buffer(96)
+        assert lib().hc_g1_decompress(bls.g1_compress(p), ob) == 0
+        assert (fe(ob.raw[:48]), fe(ob.raw[48:])) == p
