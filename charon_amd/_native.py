@@ -1,0 +1,117 @@
+"""Build and load libtbls_gpu.so (the HIP engine behind include/tbls_gpu.h).
+
+The library is built in-tree (``charon_amd/libtbls_gpu.so``) so it travels
+with the repository snapshot to the GPU box.  There is no CPU fallback: if
+the library or a gfx950 device is missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_PATH = os.path.join(PKG, "libtbls_gpu.so")
+HEADER = os.path.join(ROOT, "include", "tbls_gpu.h")
+
+
+def _hipcc():
+    for c in ("/opt/rocm/bin/hipcc", shutil.which("hipcc") or ""):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: cannot build libtbls_gpu.so")
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                  if f.endswith((".h", ".hip"))) + [HEADER]
+
+
+def is_stale():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(s) > t for s in sources())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the engine for gfx950 (hipcc, host + device)."""
+    if not force and not is_stale():
+        return LIB_PATH
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-Wno-pass-failed", os.path.join(CSRC, "tbls_engine.hip"), "-o", LIB_PATH + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+class TbgBatch(ctypes.Structure):
+    _fields_ = [
+        ("op", ctypes.c_uint32),
+        ("n_duties", ctypes.c_uint32),
+        ("n_partials", ctypes.c_uint32),
+        ("n_msgs", ctypes.c_uint32),
+        ("msgs", ctypes.c_void_p),
+        ("msg_off", ctypes.c_void_p),
+        ("duty_msg", ctypes.c_void_p),
+        ("duty_first", ctypes.c_void_p),
+        ("duty_threshold", ctypes.c_void_p),
+        ("sigs", ctypes.c_void_p),
+        ("identifiers", ctypes.c_void_p),
+        ("pubkey_ids", ctypes.c_void_p),
+    ]
+
+
+class TbgConfig(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("max_partials", ctypes.c_uint32),
+        ("max_duties", ctypes.c_uint32),
+        ("max_msg_bytes", ctypes.c_uint32),
+        ("slots", ctypes.c_uint32),
+    ]
+
+
+# exported symbols and their signatures (checked by tests/test_cabi.py)
+SIGNATURES = {
+    "tbg_init": (ctypes.c_int, [ctypes.POINTER(TbgConfig), ctypes.POINTER(ctypes.c_void_p)]),
+    "tbg_destroy": (None, [ctypes.c_void_p]),
+    "tbg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "tbg_device_count": (ctypes.c_int, []),
+    "tbg_load_pubkeys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p]),
+    "tbg_pubkey_count": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "tbg_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TbgBatch), ctypes.POINTER(ctypes.c_uint64)]),
+    "tbg_collect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_int]),
+    "tbg_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TbgBatch), ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p]),
+    "tbg_replay": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
+    "tbg_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tbg_last_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "tbg_sk_to_pk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    "tbg_sign": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the engine library (never a CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib

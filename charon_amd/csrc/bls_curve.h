@@ -52,7 +52,7 @@ template <class F> TBG_HD Jac<F> jac_from_aff(const Aff<F>& a) { return {a.x, a.
 template <class F> TBG_HD Jac<F> jac_neg(const Jac<F>& p) { return {p.X, f_reduce(f_neg(p.Y)), p.Z}; }
 
 // dbl-2009-l (a = 0). Inputs < 2p, outputs < 2p.
-template <class F> TBG_HD Jac<F> jac_dbl(const Jac<F>& p) {
+template <class F> TBG_NI Jac<F> jac_dbl(const Jac<F>& p) {
   F A = f_sqr(p.X);
   F B = f_sqr(p.Y);
   F C = f_sqr(B);
@@ -68,7 +68,7 @@ template <class F> TBG_HD Jac<F> jac_dbl(const Jac<F>& p) {
 }
 
 // add-2007-bl with the exceptional cases handled (P == Q, P == -Q, infinity).
-template <class F> TBG_HD Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+template <class F> TBG_NI Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = f_sqr(p.Z);
@@ -96,7 +96,7 @@ template <class F> TBG_HD Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // Mixed addition P (Jacobian) + Q (affine), exceptional cases handled.
-template <class F> TBG_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
+template <class F> TBG_NI Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.Z);
   F U2 = f_mul(q.x, Z1Z1);
@@ -118,7 +118,7 @@ template <class F> TBG_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   return {X3, Y3, Z3};
 }
 
-template <class F> TBG_HD bool jac_to_aff(const Jac<F>& p, Aff<F>& out) {
+template <class F> TBG_NI bool jac_to_aff(const Jac<F>& p, Aff<F>& out) {
   if (jac_is_inf(p)) return false;
   F zi = f_inv(p.Z);
   F zi2 = f_sqr(zi);
@@ -127,7 +127,7 @@ template <class F> TBG_HD bool jac_to_aff(const Jac<F>& p, Aff<F>& out) {
   return true;
 }
 
-template <class F> TBG_HD bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
+template <class F> TBG_NI bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
   bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F Z1Z1 = f_sqr(p.Z), Z2Z2 = f_sqr(q.Z);
@@ -136,7 +136,7 @@ template <class F> TBG_HD bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // [k] P for a 64-bit scalar (MSB-first double and add).
-template <class F> TBG_HD Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
+template <class F> TBG_NI Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
   Jac<F> acc = jac_inf<F>();
   bool started = false;
   for (int i = 63; i >= 0; --i) {
@@ -150,7 +150,7 @@ template <class F> TBG_HD Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
 }
 
 // [|x|] P with |x| = 0xd201000000010000 (fixed schedule: 63 doublings, 5 additions).
-template <class F> TBG_HD Jac<F> jac_mul_xabs(const Jac<F>& p) {
+template <class F> TBG_NI Jac<F> jac_mul_xabs(const Jac<F>& p) {
   Jac<F> acc = p;
   for (int i = 62; i >= 0; --i) {
     acc = jac_dbl(acc);
@@ -160,7 +160,7 @@ template <class F> TBG_HD Jac<F> jac_mul_xabs(const Jac<F>& p) {
 }
 
 // [k] P for a multi-word scalar (little-endian 32-bit words, nbits significant).
-template <class F> TBG_HD Jac<F> jac_mul_words(const Jac<F>& p, const uint32_t* w, int nbits) {
+template <class F> TBG_NI Jac<F> jac_mul_words(const Jac<F>& p, const uint32_t* w, int nbits) {
   Jac<F> acc = jac_inf<F>();
   for (int i = nbits - 1; i >= 0; --i) {
     acc = jac_dbl(acc);
@@ -180,7 +180,7 @@ TBG_HD G2J g2_psi(const G2J& p) {
 }
 
 // Subgroup membership for points on E2 (Scott 2021): P in G2 <=> psi(P) == [x] P.
-TBG_HD bool g2_in_subgroup(const G2J& p) {
+TBG_NI bool g2_in_subgroup(const G2J& p) {
   if (jac_is_inf(p)) return true;
   G2J xp = jac_neg(jac_mul_xabs(p));  // [x]P, x < 0
   return jac_eq(g2_psi(p), xp);
@@ -194,7 +194,7 @@ TBG_HD bool g2_on_curve_aff(const G2A& a) {
 
 // Budroni-Pintore cofactor clearing (RFC 9380 G.3):
 //   h(P) = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P)
-TBG_HD G2J g2_clear_cofactor(const G2J& p) {
+TBG_NI G2J g2_clear_cofactor(const G2J& p) {
   G2J t1 = jac_neg(jac_mul_xabs(p));         // [x]P
   G2J t2 = g2_psi(p);                         // psi(P)
   G2J t3 = g2_psi(g2_psi(jac_dbl(p)));        // psi^2(2P)
@@ -208,7 +208,7 @@ TBG_HD G2J g2_clear_cofactor(const G2J& p) {
 
 // ------------------------------------------------------------------ G1 extra
 // P in G1 <=> phi(P) == -[x^2] P, phi(x, y) = (beta x, y).
-TBG_HD bool g1_in_subgroup(const G1J& p) {
+TBG_NI bool g1_in_subgroup(const G1J& p) {
   if (jac_is_inf(p)) return true;
   G1J x2p = jac_mul_xabs(jac_mul_xabs(p));   // [x^2]P (x^2 > 0)
   G1J phi = {fp_mul(p.X, fp_from_const(G1_BETA)), p.Y, p.Z};
@@ -226,7 +226,7 @@ enum DecodeStatus : int32_t {
 };
 
 // 96-byte ZCash compressed G2 -> affine (Montgomery).
-TBG_HD int32_t g2_decompress(const uint8_t* b, G2A& out) {
+TBG_NI int32_t g2_decompress(const uint8_t* b, G2A& out) {
   uint32_t c_flag = (b[0] >> 7) & 1, i_flag = (b[0] >> 6) & 1, s_flag = (b[0] >> 5) & 1;
   if (!c_flag) return DEC_ERR_FLAGS;
   uint8_t hi[48];
@@ -253,7 +253,7 @@ TBG_HD int32_t g2_decompress(const uint8_t* b, G2A& out) {
 }
 
 // 48-byte ZCash compressed G1 -> affine (Montgomery).
-TBG_HD int32_t g1_decompress(const uint8_t* b, G1A& out) {
+TBG_NI int32_t g1_decompress(const uint8_t* b, G1A& out) {
   uint32_t c_flag = (b[0] >> 7) & 1, i_flag = (b[0] >> 6) & 1, s_flag = (b[0] >> 5) & 1;
   if (!c_flag) return DEC_ERR_FLAGS;
   uint8_t xb[48];

@@ -21,8 +21,12 @@
 
 #if defined(__HIP__)
 #define TBG_HD __host__ __device__ __forceinline__
+// Out-of-line on the device: shared code for the big tower/curve routines
+// keeps kernels within the instruction cache and compile times sane.
+#define TBG_NI __host__ __device__ __noinline__
 #else
 #define TBG_HD inline
+#define TBG_NI inline
 #endif
 
 #if defined(TBG_BOUNDS_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
@@ -31,6 +35,15 @@
 #define TBG_BOUND(cond, what) do { if (!(cond)) { fprintf(stderr, "bound violated: %s at %s:%d\n", what, __FILE__, __LINE__); abort(); } } while (0)
 #else
 #define TBG_BOUND(cond, what) do { } while (0)
+#endif
+
+// Work accounting (host counting build only): u32 multiply-adds issued by the
+// field layer, used to freeze the algorithmic work model (tools/count_work.py).
+#if defined(TBG_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+extern "C" unsigned long long tbg_mad_count;
+#define TBG_COUNT(n) (tbg_mad_count += (unsigned long long)(n))
+#else
+#define TBG_COUNT(n) ((void)0)
 #endif
 
 namespace tbg {
@@ -102,6 +115,7 @@ TBG_HD Fp fp_neg(const Fp& a) {
 // Valid for a < 2^390.
 TBG_HD Fp fp_reduce(const Fp& a) {
   TBG_BOUND(a.l[NL - 1] < (1u << 26), "fp_reduce a < 2^390");
+  TBG_COUNT(14);
   // top 60 bits: a >> 330  (limb 13 holds bits 364.., limb 12 bits 336.., limb 11 bits 308..)
   uint64_t t = ((uint64_t)a.l[13] << 34) | ((uint64_t)a.l[12] << 6) | (uint64_t)(a.l[11] >> 22);
   double q = (double)t * INV_PT - 1e-9;
@@ -142,6 +156,7 @@ TBG_HD Fp fp_canon(const Fp& a) { return fp_csub_p(fp_reduce(a)); }
 // Column bound: 14 (K + 1) products of < 2^56 each, so K <= 16 fits 64 bits.
 template <int K>
 TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
+  TBG_COUNT(196 * (K + 1));
   uint32_t m[NL];
   Fp r;
   uint64_t acc = 0;
@@ -201,6 +216,7 @@ TBG_HD Fp fp_mul2(const Fp& a, const Fp& b, const Fp& c, const Fp& d) {
 // Squaring: off-diagonal products once against a doubled copy.
 TBG_HD Fp fp_sqr(const Fp& a) {
   TBG_BOUND(fp_ratio_p(a) * fp_ratio_p(a) < 2048.0, "fp_sqr bound");
+  TBG_COUNT(301);
   uint32_t a2[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) a2[i] = a.l[i] << 1;
@@ -294,7 +310,7 @@ TBG_HD Fp fp_to_mont(const Fp& a) {
 
 // Exponentiation by a fixed public exponent (square and multiply, MSB first).
 template <int NBITS, int NW>
-TBG_HD Fp fp_pow_const(const Fp& a, const uint32_t (&w)[NW]) {
+TBG_NI Fp fp_pow_const(const Fp& a, const uint32_t (&w)[NW]) {
   Fp r = a;  // top bit is 1
   for (int i = NBITS - 2; i >= 0; --i) {
     r = fp_sqr(r);

@@ -25,7 +25,7 @@ TBG_HD void sha256_init(Sha256& s) {
   s.total = 0;
 }
 
-TBG_HD void sha256_block(uint32_t (&h)[8], const uint8_t* blk) {
+TBG_NI void sha256_block(uint32_t (&h)[8], const uint8_t* blk) {
   const uint32_t K[64] = {
       0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
       0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
@@ -94,7 +94,7 @@ TBG_HD void sha256_dst_prime(Sha256& s) {
 }
 
 // expand_message_xmd(msg, DST, 256): out[256]
-TBG_HD void expand_message_xmd_256(const uint8_t* msg, uint32_t msg_len, uint8_t* out) {
+TBG_NI void expand_message_xmd_256(const uint8_t* msg, uint32_t msg_len, uint8_t* out) {
   Sha256 s;
   sha256_init(s);
   for (int i = 0; i < 64; ++i) sha256_byte(s, 0);
@@ -150,7 +150,7 @@ TBG_HD void hash_to_field_fp2(const uint8_t* msg, uint32_t msg_len, Fp2& u0, Fp2
 }
 
 // Simplified SWU to E2' then the 3-isogeny to E2, output Jacobian on E2.
-TBG_HD G2J map_to_curve_g2(const Fp2& u) {
+TBG_NI G2J map_to_curve_g2(const Fp2& u) {
   Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B), Z = fp2_from_const(SSWU_Z);
   Fp2 u2 = fp2_sqr(u);
   Fp2 zu2 = fp2_mul(Z, u2);
@@ -192,7 +192,7 @@ TBG_HD G2J map_to_curve_g2(const Fp2& u) {
 }
 
 // H(m) in G2 (Jacobian).
-TBG_HD G2J hash_to_g2(const uint8_t* msg, uint32_t msg_len) {
+TBG_NI G2J hash_to_g2(const uint8_t* msg, uint32_t msg_len) {
   Fp2 u0, u1;
   hash_to_field_fp2(msg, msg_len, u0, u1);
   G2J q0 = map_to_curve_g2(u0);

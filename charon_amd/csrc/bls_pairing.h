@@ -14,7 +14,7 @@ namespace tbg {
 struct Line { Fp2 l0, l1, l4; };
 
 // T <- 2T; line through T tangent, evaluated at P (scaled by 2 Y Z^3 w^3).
-TBG_HD Line miller_dbl(G2J& T, const Fp& nxP, const Fp& yP) {
+TBG_NI Line miller_dbl(G2J& T, const Fp& nxP, const Fp& yP) {
   Fp2 A = fp2_sqr(T.X);
   Fp2 B = fp2_sqr(T.Y);
   Fp2 C = fp2_sqr(B);
@@ -36,7 +36,7 @@ TBG_HD Line miller_dbl(G2J& T, const Fp& nxP, const Fp& yP) {
 }
 
 // T <- T + Q (Q affine); line through T and Q evaluated at P (scaled by Z3 w^3).
-TBG_HD Line miller_add(G2J& T, const G2A& Q, const Fp& nxP, const Fp& yP) {
+TBG_NI Line miller_add(G2J& T, const G2A& Q, const Fp& nxP, const Fp& yP) {
   Fp2 ZZ = fp2_sqr(T.Z);
   Fp2 U2 = fp2_mul(Q.x, ZZ);
   Fp2 S2 = fp2_mul(fp2_mul(Q.y, T.Z), ZZ);
@@ -58,7 +58,7 @@ TBG_HD Line miller_add(G2J& T, const G2A& Q, const Fp& nxP, const Fp& yP) {
 
 // prod_n f_{|x|, Q_n}(P_n), conjugated for x < 0.  P, Q must not be infinity.
 template <int N>
-TBG_HD Fp12 miller_loop(const G1A (&P)[N], const G2A (&Q)[N]) {
+TBG_NI Fp12 miller_loop(const G1A (&P)[N], const G2A (&Q)[N]) {
   G2J T[N];
   Fp nxP[N];
 #pragma unroll
@@ -86,7 +86,7 @@ TBG_HD Fp12 miller_loop(const G1A (&P)[N], const G2A (&Q)[N]) {
 }
 
 // a^|x| (square and multiply over the fixed |x|)
-TBG_HD Fp12 fp12_pow_xabs(const Fp12& a) {
+TBG_NI Fp12 fp12_pow_xabs(const Fp12& a) {
   Fp12 r = a;
   for (int i = 62; i >= 0; --i) {
     r = fp12_sqr(r);
@@ -98,7 +98,7 @@ TBG_HD Fp12 fp12_pow_xabs(const Fp12& a) {
 // a^x for a in the cyclotomic subgroup (x < 0: inverse = conjugate)
 TBG_HD Fp12 cyc_pow_x(const Fp12& a) { return fp12_conj(fp12_pow_xabs(a)); }
 
-TBG_HD Fp12 final_exp(const Fp12& f) {
+TBG_NI Fp12 final_exp(const Fp12& f) {
   // easy part: f^((p^6 - 1)(p^2 + 1))
   Fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));
   t = fp12_mul(fp12_frob(fp12_frob(t)), t);
@@ -113,7 +113,7 @@ TBG_HD Fp12 final_exp(const Fp12& f) {
 }
 
 // BLS CoreVerify with prepared affine inputs: e(pk, h) * e(-g1, sig) == 1.
-TBG_HD bool bls_verify_prepared(const G1A& pk, const G2A& h, const G2A& sig) {
+TBG_NI bool bls_verify_prepared(const G1A& pk, const G2A& h, const G2A& sig) {
   G1A P[2];
   G2A Q[2];
   P[0] = pk;

@@ -61,7 +61,7 @@ TBG_HD Fp2 fp2_inv(const Fp2& a) {
 // Square root in Fp2 via two Fp exponentiations (norm method).
 // Returns false when a is not a square.  The root returned is unspecified
 // up to sign; callers fix the sign.
-TBG_HD bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
+TBG_NI bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
   Fp2 a = fp2_reduce(a_in);
   bool a1_zero = fp_is_zero(a.c1);
   if (a1_zero) {
@@ -97,7 +97,7 @@ TBG_HD bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
 }
 
 // Legendre-style square test in Fp2: a is a square iff norm(a) is a square in Fp.
-TBG_HD bool fp2_is_square(const Fp2& a) {
+TBG_NI bool fp2_is_square(const Fp2& a) {
   Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
   if (fp_is_zero(norm)) return true;
   Fp l = fp_pow_const<EXP_LEGENDRE_BITS>(norm, EXP_LEGENDRE_WORDS);
@@ -134,7 +134,7 @@ TBG_HD Fp6 fp6_reduce(const Fp6& a) { return {fp2_reduce(a.c0), fp2_reduce(a.c1)
 TBG_HD Fp6 fp6_mul_v(const Fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
 // Karatsuba (6 Fp2 products). Inputs < 8p, output < 2p.
-TBG_HD Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+TBG_NI Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
   Fp2 t0 = fp2_mul(a.c0, b.c0);
   Fp2 t1 = fp2_mul(a.c1, b.c1);
   Fp2 t2 = fp2_mul(a.c2, b.c2);
@@ -171,7 +171,7 @@ TBG_HD Fp6 fp6_mul_by_1(const Fp6& a, const Fp2& b1) {
   return {fp2_reduce(fp2_mul_xi(t0)), t1, t2};
 }
 
-TBG_HD Fp6 fp6_inv(const Fp6& a) {
+TBG_NI Fp6 fp6_inv(const Fp6& a) {
   Fp2 c0 = fp2_reduce(fp2_sub(fp2_sqr(a.c0), fp2_reduce(fp2_mul_xi(fp2_mul(a.c1, a.c2)))));
   Fp2 c1 = fp2_reduce(fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1)));
   Fp2 c2 = fp2_reduce(fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2)));
@@ -185,7 +185,7 @@ TBG_HD Fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
 TBG_HD Fp12 fp12_conj(const Fp12& a) { return {a.c0, fp6_reduce(fp6_neg(a.c1))}; }
 
 // Inputs < 4p, output < 2p.
-TBG_HD Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
+TBG_NI Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
   Fp6 t0 = fp6_mul(a.c0, b.c0);
   Fp6 t1 = fp6_mul(a.c1, b.c1);
   Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1));
@@ -195,7 +195,7 @@ TBG_HD Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
 }
 
 // Complex squaring: 2 Fp6 products.
-TBG_HD Fp12 fp12_sqr(const Fp12& a) {
+TBG_NI Fp12 fp12_sqr(const Fp12& a) {
   Fp6 t = fp6_mul(a.c0, a.c1);                                   // < 2p
   Fp6 va1 = fp6_reduce(fp6_mul_v(a.c1));
   Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, va1));      // (a0+a1)(a0+v a1)
@@ -206,7 +206,7 @@ TBG_HD Fp12 fp12_sqr(const Fp12& a) {
 }
 
 // f * (l0 + l1 v + l4 v w): the Miller-loop line (positions 0, 1, 4).
-TBG_HD Fp12 fp12_mul_by_014(const Fp12& a, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
+TBG_NI Fp12 fp12_mul_by_014(const Fp12& a, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
   Fp6 t0 = fp6_mul_by_01(a.c0, l0, l1);
   Fp6 t1 = fp6_mul_by_1(a.c1, l4);
   Fp6 s = fp6_mul_by_01(fp6_add(a.c0, a.c1), l0, fp2_add(l1, l4));
@@ -215,7 +215,7 @@ TBG_HD Fp12 fp12_mul_by_014(const Fp12& a, const Fp2& l0, const Fp2& l1, const F
   return {c0, c1};
 }
 
-TBG_HD Fp12 fp12_inv(const Fp12& a) {
+TBG_NI Fp12 fp12_inv(const Fp12& a) {
   Fp6 t = fp6_reduce(fp6_sub(fp6_mul(a.c0, a.c0), fp6_reduce(fp6_mul_v(fp6_mul(a.c1, a.c1)))));
   Fp6 ti = fp6_inv(t);
   return {fp6_mul(a.c0, ti), fp6_reduce(fp6_neg(fp6_mul(a.c1, ti)))};
@@ -224,7 +224,7 @@ TBG_HD Fp12 fp12_inv(const Fp12& a) {
 // f^p: conj every Fp2 coefficient and multiply by gamma_k = xi^(k(p-1)/6),
 // with f = sum a_k w^k, a_0 = c0.c0, a_1 = c1.c0, a_2 = c0.c1, a_3 = c1.c1,
 // a_4 = c0.c2, a_5 = c1.c2.
-TBG_HD Fp12 fp12_frob(const Fp12& a) {
+TBG_NI Fp12 fp12_frob(const Fp12& a) {
   Fp12 r;
   r.c0.c0 = fp2_reduce(fp2_conj(a.c0.c0));
   r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), fp2_from_const(FROB_G2));

@@ -1,0 +1,520 @@
+// libtbls_gpu.so: the C ABI of include/tbls_gpu.h on top of the HIP kernels.
+//
+// Per context: one HIP stream on one device, a resident public-key table,
+// and a ring of in-flight batch slots.  tbg_submit packs the caller's
+// structure-of-arrays batch into one pinned buffer, issues a single H2D copy,
+// the kernel chain and a single D2H copy of the results, then returns a
+// ticket; tbg_collect waits for (or polls) the slot's event and unpacks.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+#include "tbls_kernels.h"
+
+using namespace tbg;
+
+namespace {
+
+constexpr int kBlock = 64;
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct Slot {
+  bool busy = false;
+  bool done_collected = true;
+  tbg_ticket ticket = 0;
+  uint32_t op = 0, n_duties = 0, n_partials = 0, n_msgs = 0;
+  // pinned host staging
+  uint8_t* h_in = nullptr;
+  size_t h_in_cap = 0;
+  uint8_t* h_out = nullptr;
+  size_t h_out_cap = 0;
+  // device memory: one input arena + one work/output arena
+  uint8_t* d_in = nullptr;
+  size_t d_in_cap = 0;
+  uint8_t* d_work = nullptr;
+  size_t d_work_cap = 0;
+  size_t out_bytes = 0;
+  hipEvent_t ev[7] = {};
+  hipEvent_t done = nullptr;
+  float ms[6] = {};
+  tbg::DevBatch B{};           // device view of the last batch (resident until the slot is reused)
+  size_t w_out = 0;
+};
+
+}  // namespace
+
+struct tbg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  G1A* d_pk = nullptr;
+  int32_t* d_pk_status = nullptr;
+  uint32_t n_pk = 0, cap_pk = 0;
+  std::vector<Slot> slots;
+  tbg_ticket next_ticket = 1;
+  float last_ms[6] = {};
+};
+
+#define HIP_TRY(x)                       \
+  do {                                   \
+    hipError_t e_ = (x);                 \
+    if (e_ != hipSuccess) return TBG_E_DEVICE; \
+  } while (0)
+
+static int grow_pinned(uint8_t** p, size_t* cap, size_t need) {
+  if (*cap >= need) return TBG_OK;
+  if (*p) hipHostFree(*p);
+  *p = nullptr;
+  size_t n = align_up(need + need / 4, 1 << 20);
+  if (hipHostMalloc((void**)p, n, hipHostMallocDefault) != hipSuccess) { *cap = 0; return TBG_E_OOM; }
+  *cap = n;
+  return TBG_OK;
+}
+
+static int grow_device(uint8_t** p, size_t* cap, size_t need) {
+  if (*cap >= need) return TBG_OK;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  size_t n = align_up(need + need / 4, 1 << 20);
+  if (hipMalloc((void**)p, n) != hipSuccess) { *cap = 0; return TBG_E_OOM; }
+  *cap = n;
+  return TBG_OK;
+}
+
+extern "C" {
+
+const char* tbg_strerror(int code) {
+  switch (code) {
+    case TBG_OK: return "ok";
+    case TBG_E_INVALID_ARG: return "invalid argument";
+    case TBG_E_DEVICE: return "HIP device error";
+    case TBG_E_OOM: return "out of memory";
+    case TBG_E_NO_DEVICE: return "no gfx950 device";
+    case TBG_E_BUSY: return "all batch slots busy";
+    case TBG_E_PENDING: return "batch still running";
+    case TBG_E_TICKET: return "unknown ticket";
+    default: return "unknown error";
+  }
+}
+
+int tbg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
+  if (!out) return TBG_E_INVALID_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return TBG_E_NO_DEVICE;
+  int dev = cfg ? cfg->device : 0;
+  if (dev < 0 || dev >= ndev) return TBG_E_INVALID_ARG;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return TBG_E_DEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TBG_E_NO_DEVICE;
+  tbg_ctx* c = new (std::nothrow) tbg_ctx();
+  if (!c) return TBG_E_OOM;
+  c->device = dev;
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return TBG_E_DEVICE;
+  }
+  uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 2;
+  c->slots.resize(nslots);
+  for (auto& s : c->slots) {
+    for (auto& e : s.ev) hipEventCreate(&e);
+    hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+  }
+  *out = c;
+  return TBG_OK;
+}
+
+void tbg_destroy(tbg_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (auto& s : c->slots) {
+    if (s.h_in) hipHostFree(s.h_in);
+    if (s.h_out) hipHostFree(s.h_out);
+    if (s.d_in) hipFree(s.d_in);
+    if (s.d_work) hipFree(s.d_work);
+    for (auto& e : s.ev) hipEventDestroy(e);
+    hipEventDestroy(s.done);
+  }
+  if (c->d_pk) hipFree(c->d_pk);
+  if (c->d_pk_status) hipFree(c->d_pk_status);
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+uint32_t tbg_pubkey_count(const tbg_ctx* c) { return c ? c->n_pk : 0; }
+
+int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* first_id, int32_t* status) {
+  if (!c || (count && !pk48)) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->n_pk + (uint64_t)count > 0xFFFFFFF0ull) return TBG_E_INVALID_ARG;
+  uint32_t need = c->n_pk + count;
+  if (need > c->cap_pk) {
+    uint32_t ncap = need + need / 2 + 1024;
+    G1A* npk = nullptr;
+    int32_t* nst = nullptr;
+    if (hipMalloc(&npk, sizeof(G1A) * (size_t)ncap) != hipSuccess) return TBG_E_OOM;
+    if (hipMalloc(&nst, sizeof(int32_t) * (size_t)ncap) != hipSuccess) { hipFree(npk); return TBG_E_OOM; }
+    if (c->n_pk) {
+      HIP_TRY(hipMemcpyAsync(npk, c->d_pk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->d_pk) hipFree(c->d_pk);
+    if (c->d_pk_status) hipFree(c->d_pk_status);
+    c->d_pk = npk;
+    c->d_pk_status = nst;
+    c->cap_pk = ncap;
+  }
+  if (first_id) *first_id = c->n_pk;
+  if (count == 0) return TBG_OK;
+  uint8_t* d_bytes = nullptr;
+  if (hipMalloc(&d_bytes, 48ull * count) != hipSuccess) return TBG_E_OOM;
+  int rc = TBG_OK;
+  if (hipMemcpyAsync(d_bytes, pk48, 48ull * count, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  if (rc == TBG_OK) {
+    hipLaunchKernelGGL(k_decode_pubkeys, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, d_bytes, count,
+                       c->d_pk + c->n_pk, c->d_pk_status + c->n_pk);
+    if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
+  }
+  if (rc == TBG_OK && status &&
+      hipMemcpyAsync(status, c->d_pk_status + c->n_pk, sizeof(int32_t) * count, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+    rc = TBG_E_DEVICE;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  hipFree(d_bytes);
+  if (rc == TBG_OK) c->n_pk += count;
+  return rc;
+}
+
+// The kernel chain of one batch on the context stream; ev[0..5] bracket the
+// five kernels (decode, hash, verify, lagrange, aggregate).
+static int launch_chain(tbg_ctx* c, const DevBatch& B, hipEvent_t* ev) {
+  hipStream_t st = c->stream;
+  auto grid = [](uint32_t n) { return dim3((n + kBlock - 1) / kBlock); };
+  const uint32_t np = B.n_partials, nm = B.n_msgs, nd = B.n_duties;
+  HIP_TRY(hipEventRecord(ev[0], st));
+  if (np) hipLaunchKernelGGL(k_decode_sigs, grid(np), dim3(kBlock), 0, st, B);
+  HIP_TRY(hipEventRecord(ev[1], st));
+  if (nm) hipLaunchKernelGGL(k_hash_msgs, grid(nm), dim3(kBlock), 0, st, B);
+  HIP_TRY(hipEventRecord(ev[2], st));
+  if (B.op != TBG_OP_AGGREGATE && np)
+    hipLaunchKernelGGL(k_verify, grid(np), dim3(kBlock), 0, st, B, (const G1A*)c->d_pk, (const int32_t*)c->d_pk_status,
+                       c->n_pk);
+  HIP_TRY(hipEventRecord(ev[3], st));
+  if (B.op != TBG_OP_VERIFY && np) hipLaunchKernelGGL(k_lagrange, grid(np), dim3(kBlock), 0, st, B);
+  HIP_TRY(hipEventRecord(ev[4], st));
+  hipLaunchKernelGGL(k_aggregate, grid(nd), dim3(kBlock), 0, st, B);
+  HIP_TRY(hipEventRecord(ev[5], st));
+  HIP_TRY(hipGetLastError());
+  return TBG_OK;
+}
+
+static int validate(const tbg_batch* b) {
+  if (!b) return TBG_E_INVALID_ARG;
+  if (b->op < TBG_OP_VERIFY || b->op > TBG_OP_VERIFY_AGGREGATE) return TBG_E_INVALID_ARG;
+  if (b->n_duties == 0) return TBG_E_INVALID_ARG;
+  if (!b->duty_first || (b->n_partials && (!b->sigs || !b->identifiers))) return TBG_E_INVALID_ARG;
+  if (b->duty_first[0] != 0 || b->duty_first[b->n_duties] != b->n_partials) return TBG_E_INVALID_ARG;
+  for (uint32_t d = 0; d < b->n_duties; ++d) {
+    if (b->duty_first[d + 1] < b->duty_first[d]) return TBG_E_INVALID_ARG;
+    if (b->duty_first[d + 1] - b->duty_first[d] > 255) return TBG_E_INVALID_ARG;
+  }
+  if (b->op != TBG_OP_AGGREGATE) {
+    if (!b->msg_off || !b->duty_msg || !b->pubkey_ids || b->n_msgs == 0) return TBG_E_INVALID_ARG;
+    if (b->msg_off[0] != 0) return TBG_E_INVALID_ARG;
+    for (uint32_t m = 0; m < b->n_msgs; ++m)
+      if (b->msg_off[m + 1] < b->msg_off[m]) return TBG_E_INVALID_ARG;
+    if (b->msg_off[b->n_msgs] && !b->msgs) return TBG_E_INVALID_ARG;
+    for (uint32_t d = 0; d < b->n_duties; ++d)
+      if (b->duty_msg[d] >= b->n_msgs) return TBG_E_INVALID_ARG;
+  }
+  if (b->op == TBG_OP_VERIFY_AGGREGATE && !b->duty_threshold) return TBG_E_INVALID_ARG;
+  return TBG_OK;
+}
+
+int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
+  if (!c || !ticket) return TBG_E_INVALID_ARG;
+  int rc = validate(b);
+  if (rc != TBG_OK) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  Slot* s = nullptr;
+  for (auto& x : c->slots)
+    if (!x.busy) { s = &x; break; }
+  if (!s) return TBG_E_BUSY;
+
+  const bool verify = b->op != TBG_OP_AGGREGATE;
+  const uint32_t nd = b->n_duties, np = b->n_partials, nm = verify ? b->n_msgs : 0;
+  const size_t msg_bytes = verify ? b->msg_off[nm] : 0;
+
+  // ---- input arena layout (16-byte aligned sections) ----
+  size_t o = 0;
+  auto sec = [&](size_t bytes) { size_t at = o; o = align_up(o + bytes, 16); return at; };
+  size_t o_msgs = sec(msg_bytes);
+  size_t o_msg_off = sec(4ull * (nm + 1));
+  size_t o_duty_msg = sec(4ull * nd);
+  size_t o_duty_first = sec(4ull * (nd + 1));
+  size_t o_thr = sec(4ull * nd);
+  size_t o_pduty = sec(4ull * np);
+  size_t o_sigs = sec(96ull * np);
+  size_t o_ids = sec(np);
+  size_t o_pk = sec(4ull * np);
+  size_t in_bytes = o;
+  // ---- work/output arena ----
+  o = 0;
+  size_t w_sig_aff = sec(sizeof(G2A) * (size_t)np);
+  size_t w_h_aff = sec(sizeof(G2A) * (size_t)nm);
+  size_t w_h_st = sec(4ull * nm);
+  size_t w_lam = sec(32ull * np);
+  size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
+  size_t w_pst = sec(4ull * np);
+  size_t w_dst = sec(4ull * nd);
+  size_t w_agg = sec(96ull * nd);
+  size_t work_bytes = o;
+  size_t out_bytes = work_bytes - w_out;
+
+  if ((rc = grow_pinned(&s->h_in, &s->h_in_cap, in_bytes)) != TBG_OK) return rc;
+  if ((rc = grow_pinned(&s->h_out, &s->h_out_cap, out_bytes)) != TBG_OK) return rc;
+  if ((rc = grow_device(&s->d_in, &s->d_in_cap, in_bytes)) != TBG_OK) return rc;
+  if ((rc = grow_device(&s->d_work, &s->d_work_cap, work_bytes)) != TBG_OK) return rc;
+
+  uint8_t* h = s->h_in;
+  if (msg_bytes) memcpy(h + o_msgs, b->msgs, msg_bytes);
+  if (verify) {
+    memcpy(h + o_msg_off, b->msg_off, 4ull * (nm + 1));
+    memcpy(h + o_duty_msg, b->duty_msg, 4ull * nd);
+    memcpy(h + o_pk, b->pubkey_ids, 4ull * np);
+  }
+  memcpy(h + o_duty_first, b->duty_first, 4ull * (nd + 1));
+  if (b->op == TBG_OP_VERIFY_AGGREGATE) memcpy(h + o_thr, b->duty_threshold, 4ull * nd);
+  else memset(h + o_thr, 0, 4ull * nd);
+  uint32_t* pd = (uint32_t*)(h + o_pduty);
+  for (uint32_t d = 0; d < nd; ++d)
+    for (uint32_t j = b->duty_first[d]; j < b->duty_first[d + 1]; ++j) pd[j] = d;
+  if (np) {
+    memcpy(h + o_sigs, b->sigs, 96ull * np);
+    memcpy(h + o_ids, b->identifiers, np);
+  }
+
+  DevBatch B;
+  B.op = b->op;
+  B.n_duties = nd;
+  B.n_partials = np;
+  B.n_msgs = nm;
+  uint8_t* di = s->d_in;
+  uint8_t* dw = s->d_work;
+  B.msgs = di + o_msgs;
+  B.msg_off = (const uint32_t*)(di + o_msg_off);
+  B.duty_msg = (const uint32_t*)(di + o_duty_msg);
+  B.duty_first = (const uint32_t*)(di + o_duty_first);
+  B.duty_threshold = (const uint32_t*)(di + o_thr);
+  B.partial_duty = (const uint32_t*)(di + o_pduty);
+  B.sigs = di + o_sigs;
+  B.identifiers = di + o_ids;
+  B.pubkey_ids = (const uint32_t*)(di + o_pk);
+  B.sig_aff = (G2A*)(dw + w_sig_aff);
+  B.h_aff = (G2A*)(dw + w_h_aff);
+  B.h_status = (int32_t*)(dw + w_h_st);
+  B.lam = (uint32_t*)(dw + w_lam);
+  B.partial_status = (int32_t*)(dw + w_pst);
+  B.duty_status = (int32_t*)(dw + w_dst);
+  B.agg = dw + w_agg;
+
+  hipStream_t st = c->stream;
+  HIP_TRY(hipMemcpyAsync(s->d_in, s->h_in, in_bytes, hipMemcpyHostToDevice, st));
+  rc = launch_chain(c, B, s->ev);
+  if (rc != TBG_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(s->h_out, dw + w_out, out_bytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(s->done, st));
+
+  s->busy = true;
+  s->ticket = c->next_ticket++;
+  s->op = b->op;
+  s->n_duties = nd;
+  s->n_partials = np;
+  s->n_msgs = nm;
+  s->out_bytes = out_bytes;
+  s->B = B;
+  s->w_out = w_out;
+  *ticket = s->ticket;
+  return TBG_OK;
+}
+
+int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg, int block) {
+  if (!c) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = nullptr;
+  for (auto& x : c->slots)
+    if (x.busy && x.ticket == t) { s = &x; break; }
+  if (!s) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  if (!block) {
+    hipError_t q = hipEventQuery(s->done);
+    if (q == hipErrorNotReady) return TBG_E_PENDING;
+    if (q != hipSuccess) { s->busy = false; return TBG_E_DEVICE; }
+  } else if (hipEventSynchronize(s->done) != hipSuccess) {
+    s->busy = false;
+    return TBG_E_DEVICE;
+  }
+  const uint32_t np = s->n_partials, nd = s->n_duties;
+  size_t o = 0;
+  auto sec = [&](size_t bytes) { size_t at = o; o = align_up(o + bytes, 16); return at; };
+  size_t o_pst = sec(4ull * np), o_dst = sec(4ull * nd), o_agg = sec(96ull * nd);
+  if (pst) memcpy(pst, s->h_out + o_pst, 4ull * np);
+  if (dst) memcpy(dst, s->h_out + o_dst, 4ull * nd);
+  if (agg) memcpy(agg, s->h_out + o_agg, 96ull * nd);
+  for (int k = 0; k < 5; ++k) hipEventElapsedTime(&s->ms[k], s->ev[k], s->ev[k + 1]);
+  hipEventElapsedTime(&s->ms[5], s->ev[0], s->ev[5]);
+  memcpy(c->last_ms, s->ms, sizeof(c->last_ms));
+  s->busy = false;
+  return TBG_OK;
+}
+
+int tbg_run(tbg_ctx* c, const tbg_batch* b, int32_t* pst, int32_t* dst, uint8_t* agg) {
+  tbg_ticket t;
+  int rc = tbg_submit(c, b, &t);
+  if (rc != TBG_OK) return rc;
+  return tbg_collect(c, t, pst, dst, agg, 1);
+}
+
+int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms6) {
+  if (!c || iters == 0) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = nullptr;
+  for (auto& x : c->slots)
+    if (!x.busy && x.ticket == t) { s = &x; break; }
+  if (!s) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<hipEvent_t> ev(6ull * iters);
+  for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  int rc = TBG_OK;
+  for (uint32_t k = 0; k < iters && rc == TBG_OK; ++k) rc = launch_chain(c, s->B, ev.data() + 6ull * k);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  float acc[6] = {0, 0, 0, 0, 0, 0};
+  if (rc == TBG_OK) {
+    for (uint32_t k = 0; k < iters; ++k) {
+      hipEvent_t* e = ev.data() + 6ull * k;
+      float m;
+      for (int j = 0; j < 5; ++j) { hipEventElapsedTime(&m, e[j], e[j + 1]); acc[j] += m; }
+    }
+    hipEventElapsedTime(&acc[5], ev[0], ev[6ull * (iters - 1) + 5]);
+    if (ms6) memcpy(ms6, acc, sizeof(acc));
+    memcpy(c->last_ms, acc, sizeof(acc));
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  return rc;
+}
+
+int tbg_fetch(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg) {
+  if (!c) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = nullptr;
+  for (auto& x : c->slots)
+    if (!x.busy && x.ticket == t) { s = &x; break; }
+  if (!s) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(s->h_out, s->d_work + s->w_out, s->out_bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const uint32_t np = s->n_partials, nd = s->n_duties;
+  size_t o = 0;
+  auto sec = [&](size_t bytes) { size_t at = o; o = align_up(o + bytes, 16); return at; };
+  size_t o_pst = sec(4ull * np), o_dst = sec(4ull * nd), o_agg = sec(96ull * nd);
+  if (pst) memcpy(pst, s->h_out + o_pst, 4ull * np);
+  if (dst) memcpy(dst, s->h_out + o_dst, 4ull * nd);
+  if (agg) memcpy(agg, s->h_out + o_agg, 96ull * nd);
+  return TBG_OK;
+}
+
+int tbg_last_timings(const tbg_ctx* c, float* ms6) {
+  if (!c || !ms6) return TBG_E_INVALID_ARG;
+  memcpy(ms6, c->last_ms, sizeof(c->last_ms));
+  return TBG_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int tbg_sk_to_pk(tbg_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* pk48) {
+  if (!c || (n && (!sk32 || !pk48))) return TBG_E_INVALID_ARG;
+  if (n == 0) return TBG_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  uint8_t *d_sk = nullptr, *d_pk = nullptr;
+  if (hipMalloc(&d_sk, 32ull * n) != hipSuccess) return TBG_E_OOM;
+  if (hipMalloc(&d_pk, 48ull * n) != hipSuccess) { hipFree(d_sk); return TBG_E_OOM; }
+  int rc = TBG_OK;
+  if (hipMemcpyAsync(d_sk, sk32, 32ull * n, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  if (rc == TBG_OK) {
+    hipLaunchKernelGGL(k_sk_to_pk, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, d_sk, n, d_pk);
+    if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
+  }
+  if (rc == TBG_OK && hipMemcpyAsync(pk48, d_pk, 48ull * n, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  hipFree(d_sk);
+  hipFree(d_pk);
+  return rc;
+}
+
+int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, const uint32_t* msg_off, uint32_t n_msgs,
+             const uint32_t* item_msg, uint8_t* sig96) {
+  if (!c || (n && (!sk32 || !sig96 || !item_msg)) || n_msgs == 0 || !msg_off) return TBG_E_INVALID_ARG;
+  if (msg_off[0] != 0) return TBG_E_INVALID_ARG;
+  for (uint32_t m = 0; m < n_msgs; ++m)
+    if (msg_off[m + 1] < msg_off[m]) return TBG_E_INVALID_ARG;
+  for (uint32_t i = 0; i < n; ++i)
+    if (item_msg[i] >= n_msgs) return TBG_E_INVALID_ARG;
+  if (n == 0) return TBG_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  size_t mb = msg_off[n_msgs];
+  size_t need = align_up(32ull * n, 16) + align_up(mb + 1, 16) + align_up(4ull * (n_msgs + 1), 16) + align_up(4ull * n, 16) +
+                align_up(sizeof(G2A) * (size_t)n_msgs, 16) + align_up(4ull * n_msgs, 16) + align_up(96ull * n, 16);
+  uint8_t* base = nullptr;
+  if (hipMalloc(&base, need) != hipSuccess) return TBG_E_OOM;
+  size_t o = 0;
+  auto sec = [&](size_t bytes) { uint8_t* p = base + o; o += align_up(bytes, 16); return p; };
+  uint8_t* d_sk = sec(32ull * n);
+  uint8_t* d_msgs = sec(mb + 1);
+  uint32_t* d_off = (uint32_t*)sec(4ull * (n_msgs + 1));
+  uint32_t* d_im = (uint32_t*)sec(4ull * n);
+  G2A* d_h = (G2A*)sec(sizeof(G2A) * (size_t)n_msgs);
+  int32_t* d_hs = (int32_t*)sec(4ull * n_msgs);
+  uint8_t* d_sig = sec(96ull * n);
+  int rc = TBG_OK;
+  hipStream_t st = c->stream;
+  if (hipMemcpyAsync(d_sk, sk32, 32ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+      (mb && hipMemcpyAsync(d_msgs, msgs, mb, hipMemcpyHostToDevice, st) != hipSuccess) ||
+      hipMemcpyAsync(d_off, msg_off, 4ull * (n_msgs + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(d_im, item_msg, 4ull * n, hipMemcpyHostToDevice, st) != hipSuccess)
+    rc = TBG_E_DEVICE;
+  if (rc == TBG_OK) {
+    DevBatch B;
+    memset(&B, 0, sizeof(B));
+    B.n_msgs = n_msgs;
+    B.msgs = d_msgs;
+    B.msg_off = d_off;
+    B.h_aff = d_h;
+    B.h_status = d_hs;
+    hipLaunchKernelGGL(k_hash_msgs, dim3((n_msgs + kBlock - 1) / kBlock), dim3(kBlock), 0, st, B);
+    hipLaunchKernelGGL(k_sign, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d_sk, d_im, n, d_h, d_hs, d_sig);
+    if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
+  }
+  if (rc == TBG_OK && hipMemcpyAsync(sig96, d_sig, 96ull * n, hipMemcpyDeviceToHost, st) != hipSuccess) rc = TBG_E_DEVICE;
+  if (hipStreamSynchronize(st) != hipSuccess) rc = TBG_E_DEVICE;
+  hipFree(base);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,194 @@
+"""Python handle on one MI355X threshold-BLS engine context (libtbls_gpu.so).
+
+Thin ctypes layer over include/tbls_gpu.h: resident public keys, batched
+submit/collect of DV-duties, and GPU test-vector generation.  Arrays are
+numpy; every call goes to the HIP library (no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+
+# per-partial status (TBG_PS_*)
+PS_INVALID, PS_VALID, PS_NOT_VERIFIED = 0, 1, 2
+PS_ERR_FLAGS, PS_ERR_FIELD, PS_ERR_CURVE, PS_ERR_SUBGROUP, PS_ERR_IDENTITY, PS_ERR_PUBKEY = -1, -2, -3, -4, -5, -6
+# per-duty status (TBG_DS_*)
+DS_OK, DS_NOT_AGGREGATED = 0, 1
+DS_INSUFFICIENT, DS_INSUFFICIENT_VALID = -20, -21
+DS_AGG_TOO_FEW, DS_AGG_DUPLICATE_ID, DS_AGG_IDENTITY, DS_DECODE = -22, -23, -24, -25
+OP_VERIFY, OP_AGGREGATE, OP_VERIFY_AGGREGATE = 1, 2, 3
+NO_PUBKEY = 0xFFFFFFFF
+E_PENDING = -6
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u8(buf, width=None):
+    a = np.frombuffer(bytes(buf), dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else np.ascontiguousarray(buf, dtype=np.uint8)
+    if width is not None:
+        a = a.reshape(-1, width)
+    return np.ascontiguousarray(a)
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def pack_messages(msgs):
+    """list of bytes -> (concatenated uint8, uint32 offsets)"""
+    off = np.zeros(len(msgs) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(m) for m in msgs], dtype=np.uint64).astype(np.uint32)
+    data = np.frombuffer(b"".join(msgs) + b"\0", dtype=np.uint8)
+    return np.ascontiguousarray(data), off
+
+
+@dataclass
+class BatchResult:
+    partial_status: np.ndarray  # int32 [n_partials]
+    duty_status: np.ndarray     # int32 [n_duties]
+    agg: np.ndarray             # uint8 [n_duties, 96]
+
+
+class Engine:
+    """One context = one GPU (HIP device ordinal)."""
+
+    def __init__(self, device: int = 0, slots: int = 2):
+        self._lib = _native.load()
+        cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots)
+        h = ctypes.c_void_p()
+        rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
+        self._check(rc, "tbg_init")
+        self._h = h
+        self.device = device
+        self._keep = {}
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise EngineError(f"{what}: {self._lib.tbg_strerror(rc).decode()} ({rc})")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.tbg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ pubkeys
+    def load_pubkeys(self, pk48) -> tuple[int, np.ndarray]:
+        a = _u8(pk48, 48)
+        n = a.shape[0]
+        first = ctypes.c_uint32()
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self._lib.tbg_load_pubkeys(self._h, _ptr(a), n, ctypes.byref(first), _ptr(st)), "tbg_load_pubkeys")
+        return first.value, st
+
+    @property
+    def pubkey_count(self) -> int:
+        return self._lib.tbg_pubkey_count(self._h)
+
+    # ------------------------------------------------------------ batches
+    def _batch(self, op, duty_first, sigs, identifiers, msgs=None, duty_msg=None, pubkey_ids=None, duty_threshold=None):
+        duty_first = _u32(duty_first)
+        sigs = _u8(sigs, 96) if len(sigs) else np.zeros((0, 96), np.uint8)
+        identifiers = np.ascontiguousarray(np.asarray(identifiers, dtype=np.uint8))
+        nd = len(duty_first) - 1
+        np_ = sigs.shape[0]
+        keep = [duty_first, sigs, identifiers]
+        b = _native.TbgBatch()
+        b.op, b.n_duties, b.n_partials = op, nd, np_
+        b.duty_first, b.sigs, b.identifiers = _ptr(duty_first), _ptr(sigs), _ptr(identifiers)
+        if op != OP_AGGREGATE:
+            data, off = msgs if isinstance(msgs, tuple) else pack_messages(msgs)
+            data, off = _u8(data), _u32(off)
+            duty_msg = _u32(duty_msg)
+            pubkey_ids = _u32(pubkey_ids)
+            keep += [data, off, duty_msg, pubkey_ids]
+            b.n_msgs = len(off) - 1
+            b.msgs, b.msg_off, b.duty_msg, b.pubkey_ids = _ptr(data), _ptr(off), _ptr(duty_msg), _ptr(pubkey_ids)
+        if op == OP_VERIFY_AGGREGATE:
+            duty_threshold = _u32(duty_threshold)
+            keep.append(duty_threshold)
+            b.duty_threshold = _ptr(duty_threshold)
+        return b, keep, nd, np_
+
+    def submit(self, op, duty_first, sigs, identifiers, **kw):
+        b, keep, nd, np_ = self._batch(op, duty_first, sigs, identifiers, **kw)
+        t = ctypes.c_uint64()
+        self._check(self._lib.tbg_submit(self._h, ctypes.byref(b), ctypes.byref(t)), "tbg_submit")
+        self._keep[t.value] = (nd, np_)
+        return t.value
+
+    def collect(self, ticket, block=True):
+        nd, np_ = self._keep[ticket]
+        ps = np.zeros(np_, dtype=np.int32)
+        ds = np.zeros(nd, dtype=np.int32)
+        agg = np.zeros((nd, 96), dtype=np.uint8)
+        rc = self._lib.tbg_collect(self._h, ticket, _ptr(ps), _ptr(ds), _ptr(agg), 1 if block else 0)
+        if rc == E_PENDING:
+            return None
+        del self._keep[ticket]
+        self._check(rc, "tbg_collect")
+        return BatchResult(ps, ds, agg)
+
+    def run(self, op, duty_first, sigs, identifiers, **kw) -> BatchResult:
+        return self.collect(self.submit(op, duty_first, sigs, identifiers, **kw))
+
+    def replay(self, ticket, iters=1):
+        """Re-run a collected batch's kernel chain on its resident inputs."""
+        ms = np.zeros(6, dtype=np.float32)
+        self._check(self._lib.tbg_replay(self._h, ticket, iters, _ptr(ms)), "tbg_replay")
+        return dict(zip(["decode", "hash", "verify", "lagrange", "aggregate", "total"], ms.tolist()))
+
+    def fetch(self, ticket, n_duties, n_partials) -> BatchResult:
+        ps = np.zeros(n_partials, dtype=np.int32)
+        ds = np.zeros(n_duties, dtype=np.int32)
+        agg = np.zeros((n_duties, 96), dtype=np.uint8)
+        self._check(self._lib.tbg_fetch(self._h, ticket, _ptr(ps), _ptr(ds), _ptr(agg)), "tbg_fetch")
+        return BatchResult(ps, ds, agg)
+
+    def timings(self):
+        ms = np.zeros(6, dtype=np.float32)
+        self._check(self._lib.tbg_last_timings(self._h, _ptr(ms)), "tbg_last_timings")
+        return dict(zip(["decode", "hash", "verify", "lagrange", "aggregate", "total"], ms.tolist()))
+
+    # ------------------------------------------------------------ vector generation
+    def sk_to_pk(self, sk32) -> np.ndarray:
+        a = _u8(sk32, 32)
+        out = np.zeros((a.shape[0], 48), dtype=np.uint8)
+        self._check(self._lib.tbg_sk_to_pk(self._h, _ptr(a), a.shape[0], _ptr(out)), "tbg_sk_to_pk")
+        return out
+
+    def sign(self, sk32, msgs, item_msg) -> np.ndarray:
+        a = _u8(sk32, 32)
+        data, off = msgs if isinstance(msgs, tuple) else pack_messages(msgs)
+        data, off, im = _u8(data), _u32(off), _u32(item_msg)
+        out = np.zeros((a.shape[0], 96), dtype=np.uint8)
+        self._check(self._lib.tbg_sign(self._h, _ptr(a), a.shape[0], _ptr(data), _ptr(off), len(off) - 1, _ptr(im),
+                                       _ptr(out)), "tbg_sign")
+        return out
+
+
+_default = {}
+
+
+def default_engine(device: int | None = None) -> Engine:
+    import os
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+    if device not in _default:
+        _default[device] = Engine(device)
+    return _default[device]

@@ -1,0 +1,144 @@
+/*
+ * tbls_gpu.h -- C ABI of the MI355X threshold-BLS engine (libtbls_gpu.so).
+ *
+ * Drop-in boundary for Charon's threshold-BLS hot path (singhhp1069/charon):
+ *   tbls.Verify              reference tbls/tss.go:190-197
+ *   tbls.Aggregate           reference tbls/tss.go:142-149
+ *   tbls.VerifyAndAggregate  reference tbls/tss.go:153-187
+ *   tblsconv.SigFromCore     reference tbls/tblsconv/tblsconv.go:125-132 (G2 decode, done on the GPU)
+ *   tblsconv.SigToCore       reference tbls/tblsconv/tblsconv.go:119-122     (G2 encode, done on the GPU)
+ *   tblsconv.KeyFromBytes    reference tbls/tblsconv/tblsconv.go:30-37       (G1 decode, tbg_load_pubkeys)
+ * plus the batch entry points the new batch-aware call sites use
+ * (core/parsigex/parsigex.go:101-107, core/validatorapi/validatorapi.go:228-287,
+ *  core/parsigdb/memory.go:96-134 -> core/sigagg/sigagg.go:53-103).
+ *
+ * Plain C: pointers and sizes only.  All input buffers are caller-owned and
+ * copied into pinned staging inside tbg_submit, so nothing is retained after
+ * the call returns (cgo pointer rules).  Output buffers are caller-owned and
+ * filled by tbg_collect.  One context drives one GPU; contexts are
+ * thread-safe (an internal mutex serialises submit/collect).
+ */
+#ifndef TBLS_GPU_H
+#define TBLS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- call-level return codes ------------------------------------------ */
+#define TBG_OK 0
+#define TBG_E_INVALID_ARG (-1)  /* malformed batch (bad offsets, ids, sizes)   */
+#define TBG_E_DEVICE (-2)       /* HIP runtime / kernel failure                */
+#define TBG_E_OOM (-3)          /* device or pinned allocation failed          */
+#define TBG_E_NO_DEVICE (-4)    /* no usable gfx950 device                     */
+#define TBG_E_BUSY (-5)         /* every in-flight slot is taken               */
+#define TBG_E_PENDING (-6)      /* tbg_collect(block=0): not finished yet      */
+#define TBG_E_TICKET (-7)       /* unknown or already collected ticket         */
+
+/* ---- per-partial-signature status (int32) ------------------------------ */
+#define TBG_PS_INVALID 0         /* valid encodings, pairing check false: Go (false, nil) */
+#define TBG_PS_VALID 1           /* pairing check true                                     */
+#define TBG_PS_NOT_VERIFIED 2    /* decoded fine, op did not verify (TBG_OP_AGGREGATE)     */
+#define TBG_PS_ERR_FLAGS (-1)    /* compression flag missing / bad infinity encoding       */
+#define TBG_PS_ERR_FIELD (-2)    /* x coordinate >= p                                      */
+#define TBG_PS_ERR_CURVE (-3)    /* not on the curve                                       */
+#define TBG_PS_ERR_SUBGROUP (-4) /* not in the prime-order subgroup                        */
+#define TBG_PS_ERR_IDENTITY (-5) /* signature is the point at infinity                     */
+#define TBG_PS_ERR_PUBKEY (-6)   /* pubkey id unknown / pubkey invalid or identity         */
+
+/* ---- per-duty status (int32) ------------------------------------------- */
+#define TBG_DS_OK 0
+#define TBG_DS_INSUFFICIENT (-20)        /* "insufficient signatures"        (tss.go:154-156) */
+#define TBG_DS_INSUFFICIENT_VALID (-21)  /* "insufficient valid signatures"  (tss.go:176-178) */
+#define TBG_DS_AGG_TOO_FEW (-22)         /* CombineSignatures: < 2 partials                   */
+#define TBG_DS_AGG_DUPLICATE_ID (-23)    /* CombineSignatures: identifiers collide            */
+#define TBG_DS_AGG_IDENTITY (-24)        /* CombineSignatures: identity input or result       */
+#define TBG_DS_DECODE (-25)              /* a partial failed to decode (SigFromCore error)    */
+#define TBG_DS_NOT_AGGREGATED 1          /* TBG_OP_VERIFY: no aggregate produced              */
+
+#define TBG_NO_PUBKEY 0xFFFFFFFFu        /* pubkey_ids[] entry: identifier not in the TSS     */
+
+typedef enum {
+  TBG_OP_VERIFY = 1,           /* per partial: CoreVerify(pk, msg(duty), sig)                 */
+  TBG_OP_AGGREGATE = 2,        /* per duty: CombineSignatures(all partials), no verification  */
+  TBG_OP_VERIFY_AGGREGATE = 3  /* per duty: VerifyAndAggregate(tss, partials, msg)            */
+} tbg_op;
+
+typedef struct tbg_ctx tbg_ctx;
+typedef uint64_t tbg_ticket;
+
+typedef struct {
+  int32_t device;         /* HIP device ordinal                           */
+  uint32_t max_partials;  /* staging capacity hint (grows on demand)       */
+  uint32_t max_duties;
+  uint32_t max_msg_bytes;
+  uint32_t slots;         /* in-flight batches (0 -> 2)                    */
+} tbg_config;
+
+/* A batch of DV-duties in structure-of-arrays form.
+ * Duty d owns partials [duty_first[d], duty_first[d+1]) and message duty_msg[d];
+ * message m is msgs[msg_off[m] .. msg_off[m+1]). */
+typedef struct {
+  uint32_t op;                     /* tbg_op                                          */
+  uint32_t n_duties;
+  uint32_t n_partials;
+  uint32_t n_msgs;
+  const uint8_t* msgs;             /* concatenated message bytes (VERIFY*)            */
+  const uint32_t* msg_off;         /* [n_msgs + 1]                                    */
+  const uint32_t* duty_msg;        /* [n_duties]     (VERIFY*)                        */
+  const uint32_t* duty_first;      /* [n_duties + 1]                                  */
+  const uint32_t* duty_threshold;  /* [n_duties]     (VERIFY_AGGREGATE)               */
+  const uint8_t* sigs;             /* [n_partials * 96] ZCash-compressed G2           */
+  const uint8_t* identifiers;      /* [n_partials] share index (Lagrange x)           */
+  const uint32_t* pubkey_ids;      /* [n_partials] resident pubkey id (VERIFY*)       */
+} tbg_batch;
+
+int tbg_init(const tbg_config* cfg, tbg_ctx** out);
+void tbg_destroy(tbg_ctx* ctx);
+const char* tbg_strerror(int code);
+int tbg_device_count(void);
+
+/* Decode and validate `count` 48-byte compressed G1 public keys on the GPU
+ * and append them to the resident table.  Ids are first_id .. first_id+count-1.
+ * status[i] (optional) receives 0 valid, 1 identity, or a TBG_PS_ERR_* code. */
+int tbg_load_pubkeys(tbg_ctx* ctx, const uint8_t* pk48, uint32_t count, uint32_t* first_id, int32_t* status);
+uint32_t tbg_pubkey_count(const tbg_ctx* ctx);
+
+/* Enqueue a batch (copies every input); returns a ticket. */
+int tbg_submit(tbg_ctx* ctx, const tbg_batch* batch, tbg_ticket* ticket);
+
+/* Collect a batch: partial_status [n_partials], duty_status [n_duties],
+ * agg96 [n_duties * 96] (any may be NULL).  block = 0 polls. */
+int tbg_collect(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status,
+                uint8_t* agg96, int block);
+
+/* Convenience: submit + blocking collect. */
+int tbg_run(tbg_ctx* ctx, const tbg_batch* batch, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
+
+/* Device-resident replay: re-run the kernel chain of a collected batch whose
+ * inputs are still resident in its slot's HBM arena (valid until the slot is
+ * reused by a later tbg_submit), `iters` times back to back, no host copies.
+ * Blocks; ms6 receives per-kernel totals as in tbg_last_timings.  tbg_fetch
+ * copies that slot's current outputs back (synchronous). */
+int tbg_replay(tbg_ctx* ctx, tbg_ticket ticket, uint32_t iters, float* ms6);
+int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
+
+/* Test-vector / benchmark-input generation on the GPU (not on the hot path):
+ * tbls.Sign / PartialSign (reference tbls/tss.go:200-217) and
+ * SecretKey.GetPublicKey.  sk32: 32-byte big-endian secret scalars (< r).
+ * tbg_sign signs item i with sk32[i] over message item_msg[i]. */
+int tbg_sk_to_pk(tbg_ctx* ctx, const uint8_t* sk32, uint32_t n, uint8_t* pk48);
+int tbg_sign(tbg_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, const uint32_t* msg_off,
+             uint32_t n_msgs, const uint32_t* item_msg, uint8_t* sig96);
+
+/* Last kernel timings of the context (milliseconds, HIP events on the
+ * engine's stream): [decode, hash, verify, lagrange, aggregate, total]. */
+int tbg_last_timings(const tbg_ctx* ctx, float* ms6);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TBLS_GPU_H */

@@ -11,6 +11,12 @@
 
 using namespace tbg;
 
+#if defined(TBG_COUNT_OPS)
+extern "C" unsigned long long tbg_mad_count = 0;
+extern "C" unsigned long long hc_count_get(void) { return tbg_mad_count; }
+extern "C" void hc_count_reset(void) { tbg_mad_count = 0; }
+#endif
+
 static Fp from_be(const uint8_t* b) {
   bool lt;
   return fp_to_mont(fp_limbs_from_be48(b, &lt));
@@ -116,4 +122,51 @@ int hc_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t len, const uint8
   return bls_verify_prepared(pk, ha, sig) ? 1 : 0;
 }
 
+// Work-model probes: each runs one item of a pipeline stage.
+int hc_stage_decode_sig(const uint8_t* sig96) {
+  G2A a;
+  return g2_decompress(sig96, a);
+}
+int hc_stage_verify(const uint8_t* pk48, const uint8_t* sig96, const uint8_t* msg, uint32_t len) {
+  G1A pk;
+  G2A sig, ha;
+  g1_decompress(pk48, pk);
+  g2_decompress(sig96, sig);
+  G2J h = hash_to_g2(msg, len);
+  jac_to_aff(h, ha);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  return bls_verify_prepared(pk, ha, sig) ? 1 : 0;
+}
+void hc_stage_hash(const uint8_t* msg, uint32_t len) {
+  G2J h = hash_to_g2(msg, len);
+  G2A a;
+  jac_to_aff(h, a);
+}
+
 }  // extern "C"
+
+#include "../../charon_amd/csrc/bls_tss.h"
+extern "C" {
+// Aggregate k decoded partials exactly as k_aggregate does (Lagrange + Straus).
+int hc_stage_aggregate(const uint8_t* ids, const uint8_t* sigs96, int k, uint8_t* out96) {
+  G2A pts[16];
+  uint32_t lam[16][8];
+  if (k > 16) return -1;
+  for (int i = 0; i < k; ++i)
+    if (g2_decompress(sigs96 + 96 * i, pts[i]) != DEC_OK) return -2;
+  for (int i = 0; i < k; ++i)
+    if (!lagrange_at_zero_words(ids, k, i, lam[i])) return -3;
+  G2J acc = jac_inf<Fp2>();
+  for (int bit = 254; bit >= 0; --bit) {
+    acc = jac_dbl(acc);
+    for (int j = 0; j < k; ++j)
+      if ((lam[j][bit >> 5] >> (bit & 31)) & 1) acc = jac_add_aff(acc, pts[j]);
+  }
+  G2A a;
+  bool ok = jac_to_aff(acc, a);
+  g2_compress(a, !ok, out96);
+  return ok ? 0 : -4;
+}
+}

@@ -1,0 +1,157 @@
+"""GPU parity: the HIP engine (through the C ABI) against the oracle's golden
+fixtures and against size-independent properties at full batch sizes.
+
+Bar: bit-exact 96-byte aggregates and identical accept/reject (and error
+class) on every partial signature."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+PS_NAMES = {1: "valid", 0: "invalid", -1: "err_flags", -2: "err_field", -3: "err_curve", -4: "err_subgroup",
+            -5: "err_identity", -6: "err_pubkey"}
+DS_NAMES = {0: "ok", -20: "insufficient", -21: "insufficient_valid", -22: "too_few", -23: "duplicate",
+            -24: "identity", -25: "decode"}
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)["vectors"]
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from charon_amd import engine as eng
+    e = eng.Engine(0)
+    yield e
+    e.close()
+
+
+def test_native_library_is_the_hip_engine(engine):
+    from charon_amd import _native
+    assert os.path.exists(_native.LIB_PATH)
+    assert engine._lib._name == _native.LIB_PATH
+
+
+def test_kat_verify(engine):
+    from charon_amd import tbls
+    vecs = load("kat_verify.json")
+    items = [(tbls.PublicKey(bytes.fromhex(v["pk"])), bytes.fromhex(v["msg"]), tbls.Signature(bytes.fromhex(v["sig"])))
+             for v in vecs]
+    got = tbls.verify_batch(items, engine)
+    assert got == [v["expect"] == "valid" for v in vecs]
+    # single-item Go-API form
+    assert tbls.verify(*items[0], engine=engine) is True
+
+
+def _va_batch(engine, vecs):
+    from charon_amd import tbls
+    duties = []
+    for v in vecs:
+        t = v["tss"]
+        tss = tbls.TSS({int(k): tbls.PublicKey(bytes.fromhex(pk)) for k, pk in t["pubshares"].items()},
+                       t["num_shares"], t["threshold"], tbls.PublicKey(bytes.fromhex(t["public_key"])))
+        parts = [tbls.PartialSignature(p["identifier"], tbls.Signature(bytes.fromhex(p["sig"]))) for p in v["partials"]]
+        duties.append({"tss": tss, "partials": parts, "msg": bytes.fromhex(v["msg"])})
+    return duties
+
+
+@pytest.mark.parametrize("name", ["cfg1_3of4_single.json", "cfg2_3of4_sample.json", "cfg3_7of10_sample.json",
+                                  "cfg5_mixed_invalid.json"])
+def test_verify_and_aggregate_golden(engine, name):
+    from charon_amd import engine as eng, tbls
+    vecs = load(name)
+    duties = _va_batch(engine, vecs)
+    # raw engine call: per-partial status + per-duty status + bytes
+    from charon_amd.tbls import _duty_arrays, _pk_cache
+    duty_first, sigs, ids, msgs, thr, pk_keys = _duty_arrays(duties, True)
+    present = [k for k in pk_keys if k is not None]
+    it = iter(_pk_cache.ids_for(engine, present))
+    pk_ids = [next(it) if k is not None else eng.NO_PUBKEY for k in pk_keys]
+    res = engine.run(eng.OP_VERIFY_AGGREGATE, duty_first, sigs, ids, msgs=msgs, duty_msg=np.arange(len(duties)),
+                     pubkey_ids=pk_ids, duty_threshold=thr)
+    for d, v in enumerate(vecs):
+        lo, hi = duty_first[d], duty_first[d + 1]
+        got_ps = [PS_NAMES[s] for s in res.partial_status[lo:hi].tolist()]
+        exp = v["expect"]
+        # a duty rejected for too few partials is decided before verification
+        if exp["status"] != "insufficient":
+            assert got_ps == exp["partial_status"], v["label"]
+        assert DS_NAMES[int(res.duty_status[d])] == exp["status"], v["label"]
+        if exp["status"] == "ok":
+            assert bytes(res.agg[d]).hex() == exp["agg"], v["label"]
+            assert bytes(res.agg[d]).hex() == exp["group_sig"]
+    # Go-API mirror form
+    out = tbls.verify_and_aggregate_batch(duties, engine)
+    for r, v in zip(out, vecs):
+        if v["expect"]["status"] == "ok":
+            sig, signers = r
+            assert sig.raw.hex() == v["expect"]["agg"] and signers == v["expect"]["signers"]
+        else:
+            assert isinstance(r, tbls.TblsError)
+
+
+def test_aggregate_golden(engine):
+    from charon_amd import engine as eng, tbls
+    vecs = load("aggregate_edges.json")
+    duties = [[tbls.PartialSignature(p["identifier"], tbls.Signature(bytes.fromhex(p["sig"]))) for p in v["partials"]]
+              for v in vecs]
+    duty_first = np.cumsum([0] + [len(d) for d in duties])
+    sigs = b"".join(p.signature.raw for d in duties for p in d)
+    ids = [p.identifier for d in duties for p in d]
+    res = engine.run(eng.OP_AGGREGATE, duty_first, sigs, ids)
+    for d, v in enumerate(vecs):
+        assert DS_NAMES[int(res.duty_status[d])] == v["expect"]["status"], v["label"]
+        if v["expect"]["status"] == "ok":
+            assert bytes(res.agg[d]).hex() == v["expect"]["agg"], v["label"]
+    # Go-API mirror
+    for d, v in zip(duties, vecs):
+        if v["expect"]["status"] == "ok":
+            assert tbls.aggregate(d, engine).raw.hex() == v["expect"]["agg"]
+        else:
+            with pytest.raises(tbls.TblsError):
+                tbls.aggregate(d, engine)
+
+
+def test_engine_sign_matches_oracle(engine):
+    """GPU test-vector generation (tbls.Sign) agrees with the oracle."""
+    from oracle import bls12_381 as bls
+    from oracle import tbls_oracle as tb
+    rng = random.Random(7)
+    sks = [rng.randrange(1, bls.R) for _ in range(3)]
+    msgs = [b"Hello Obol", bytes(32), bytes(range(32))]
+    sk32 = b"".join(s.to_bytes(32, "big") for s in sks)
+    sigs = engine.sign(sk32, msgs, [0, 1, 2])
+    pks = engine.sk_to_pk(sk32)
+    for i, s in enumerate(sks):
+        assert bytes(sigs[i]) == bls.g2_compress(tb.sign(s, msgs[i]))
+        assert bytes(pks[i]) == bls.g1_compress(tb.sk_to_pk(s))
+
+
+def _make_cluster_batch(engine, n_dv, t, n, seed, inject=0.0):
+    """Full-size synthetic batch built on the GPU (keys, shares, signatures)."""
+    from tools.workload import make_batch
+    return make_batch(engine, n_dv, t, n, seed, inject=inject)
+
+
+@pytest.mark.parametrize("n_dv,t,n", [(2000, 3, 4), (300, 7, 10)])
+def test_full_size_properties(engine, n_dv, t, n):
+    """At batch scale: every honest partial verifies, every aggregate equals
+    the group signature sk * H(m) computed independently on the GPU, and an
+    injected invalid partial is rejected without changing the aggregate."""
+    from charon_amd import engine as eng
+    b = _make_cluster_batch(engine, n_dv, t, n, seed=11, inject=0.02)
+    res = engine.run(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
+                     duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+    expect_valid = ~b.injected
+    assert np.array_equal(res.partial_status == eng.PS_VALID, expect_valid)
+    ok = res.duty_status == eng.DS_OK
+    assert np.array_equal(ok, b.expect_ok)
+    assert np.array_equal(res.agg[ok], b.group_sig[ok])

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Freeze the algorithmic work model of the engine's per-item schedule.
+
+Builds the host copy of the device math with TBG_COUNT_OPS (every Montgomery
+product / square / reduction adds its u32 multiply-add count) and measures
+one item of each pipeline stage on real inputs from the golden fixtures.
+Writes profiles/work_model.json, which bench.py uses for roofline.achieved.
+One Fp multiplication = 392 u32 mul-adds in this radix-2^28 schedule
+(196 a*b + 196 m*p); the survey's 12x32-bit CIOS figure is 300.
+"""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SRC = os.path.join(ROOT, "tests", "hostcheck", "hostcheck.cpp")
+LIB = os.path.join(ROOT, "tests", "hostcheck", "libhostcheck_count.so")
+
+
+def main():
+    subprocess.check_call(["/opt/rocm/llvm/bin/clang++", "-O1", "-std=c++17", "-fPIC", "-shared", "-DTBG_COUNT_OPS",
+                           "-Wno-pass-failed", SRC, "-o", LIB])
+    lib = ctypes.CDLL(LIB)
+    lib.hc_count_get.restype = ctypes.c_ulonglong
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "cfg1_3of4_single.json")))["vectors"][0]
+    msg = bytes.fromhex(gold["msg"])
+    sigs = [bytes.fromhex(p["sig"]) for p in gold["partials"]]
+    pks = [bytes.fromhex(gold["tss"]["pubshares"][str(p["identifier"])]) for p in gold["partials"]]
+
+    def measure(fn, *a):
+        lib.hc_count_reset()
+        r = fn(*a)
+        return lib.hc_count_get(), r
+
+    decode, st = measure(lib.hc_stage_decode_sig, sigs[0])
+    assert st == 0
+    hash_, _ = measure(lib.hc_stage_hash, msg, len(msg))
+    lib.hc_count_reset()
+    assert lib.hc_stage_verify(pks[0], sigs[0], msg, len(msg)) == 1
+    verify = lib.hc_count_get()
+    out = ctypes.create_string_buffer(96)
+    ids = bytes([p["identifier"] for p in gold["partials"]])
+    lib.hc_count_reset()
+    assert lib.hc_stage_aggregate(ids, b"".join(sigs), len(sigs), out) == 0
+    agg_with_decode = lib.hc_count_get()
+    assert out.raw.hex() == gold["expect"]["agg"]
+    agg = agg_with_decode - len(sigs) * decode
+    unit_3of4 = 4 * decode + hash_ + 4 * verify + agg
+    model = {
+        "generator": "tools/count_work.py",
+        "mads_per_fp_mul": 392,
+        "mads": {"decode_sig": decode, "hash_to_g2": hash_, "verify_item": verify, "aggregate_3of4_all4": agg,
+                 "unit_3of4": unit_3of4},
+        "fp_mul_equiv": {k: round(v / 392, 1) for k, v in
+                         {"decode_sig": decode, "hash_to_g2": hash_, "verify_item": verify,
+                          "aggregate_3of4_all4": agg, "unit_3of4": unit_3of4}.items()},
+        "verify_hbm_bytes_per_launch": None,
+    }
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "work_model.json"), "w") as f:
+        json.dump(model, f, indent=1)
+    print(json.dumps(model, indent=1))
+
+
+if __name__ == "__main__":
+    main()
