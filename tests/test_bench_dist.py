@@ -1,0 +1,50 @@
+"""bench.py's multi-process plumbing (barrier, max-over-ranks timing, weak
+scaling value) with world_size 2 on the gloo backend (CPU)."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), TBG_DIST_BACKEND="gloo")
+    import time
+    import bench
+    w, r, _ = bench.dist_setup()
+    assert (w, r) == (ws, rank)
+
+    def step(k):
+        time.sleep(0.05 * (rank + 1) * k)  # rank 1 is slower: max over ranks must see it
+        return k
+
+    dt, out = bench.timed_steps(step, 2, ws)
+    q.put((rank, dt, out))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_two_rank_max_over_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dts = {r: dt for r, dt, _ in res}
+    # both ranks report the same (max) elapsed time, at least the slow rank's 0.2 s
+    assert abs(dts[0] - dts[1]) < 1e-9
+    assert dts[0] >= 0.2

@@ -1,0 +1,58 @@
+"""The C-ABI library loads and exports every entry point include/tbls_gpu.h
+declares (no compute without a GPU), and fails loudly without a device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tbls_gpu.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\s*\*|uint32_t)\s+(tbg_\w+)\s*\(", src, re.M)))
+
+
+def lib_path():
+    from charon_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libtbls_gpu.so not built (run __graft_entry__.build())")
+    return _native.LIB_PATH
+
+
+def test_header_declares_the_boundary():
+    names = declared()
+    for must in ["tbg_init", "tbg_destroy", "tbg_load_pubkeys", "tbg_submit", "tbg_collect", "tbg_run",
+                 "tbg_replay", "tbg_fetch", "tbg_strerror", "tbg_sign", "tbg_sk_to_pk"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(lib_path())
+    missing = [n for n in declared() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_the_header():
+    from charon_amd import _native
+    assert set(declared()) == set(_native.SIGNATURES)
+
+
+def test_strerror_without_gpu():
+    from charon_amd import _native
+    lib = _native.load() if os.path.exists(_native.LIB_PATH) else pytest.skip("not built")
+    assert lib.tbg_strerror(0) == b"ok"
+    assert lib.tbg_strerror(-4) == b"no gfx950 device"
+
+
+def test_no_cpu_fallback_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from charon_amd import _native, engine
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("not built")
+    with pytest.raises(engine.EngineError):
+        engine.Engine(0)
