@@ -144,10 +144,10 @@ def main():
     roofline = None
     if wm:
         key = f"{args.t}of{args.n}"
-        per_verify = wm["mads"]["verify_item"]
+        per_verify = wm["mads"]["verify_quad_item"]
         verify_ms = kernel_ms["verify"] / args.steps
         achieved = per_verify * args.dvs * args.n / (verify_ms * 1e-3) / 1e12
-        roofline = {"bound": "valu-int-mul", "kernel": "k_verify", "achieved": round(achieved, 3),
+        roofline = {"bound": "valu-int-mul", "kernel": "k_verify_quad", "achieved": round(achieved, 3),
                     "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s", "frac": round(achieved / PEAK_MAD_TOPS, 4),
                     "traffic": wm.get("verify_hbm_bytes_per_launch"),
                     "work_per_unit_mads": wm["mads"].get("unit_" + key)}

@@ -37,17 +37,38 @@ def is_stale():
     return any(os.path.getmtime(s) > t for s in sources())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile the engine for gfx950 (hipcc, host + device)."""
-    if not force and not is_stale():
+def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(), out: str | None = None) -> str:
+    """Compile the engine for gfx950: every csrc/*.hip translation unit in
+    parallel (hipcc -c), then link libtbls_gpu.so.  `defines` / `out` build a
+    tuning variant elsewhere (tools/ab_variants.py)."""
+    target = out or LIB_PATH
+    if not force and out is None and not is_stale():
         return LIB_PATH
-    cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wno-pass-failed", os.path.join(CSRC, "tbls_engine.hip"), "-o", LIB_PATH + ".tmp"]
+    from concurrent.futures import ThreadPoolExecutor
+    hipcc = _hipcc()
+    units = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
+    objdir = os.path.join(PKG, "build_obj", os.path.basename(target).replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed", "-Wno-unused-result"]
+    flags += ["-D" + d for d in defines]
+
+    def compile_unit(u):
+        obj = os.path.join(objdir, u.replace(".hip", ".o"))
+        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, u), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        return obj
+
+    jobs = jobs or min(len(units), max(1, (os.cpu_count() or 4)), 8)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_unit, units))
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", target + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(target + ".tmp", target)
+    return target
 
 
 class TbgBatch(ctypes.Structure):
@@ -106,9 +127,10 @@ def load() -> ctypes.CDLL:
     """Load the engine library (never a CPU fallback)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
-        lib = ctypes.CDLL(LIB_PATH)
+        path = os.environ.get("TBG_LIB", LIB_PATH)  # tuning variants only (tools/ab_variants.py)
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+        lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res

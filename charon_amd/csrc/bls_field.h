@@ -23,7 +23,7 @@
 #define TBG_HD __host__ __device__ __forceinline__
 // Out-of-line on the device: shared code for the big tower/curve routines
 // keeps kernels within the instruction cache and compile times sane.
-#define TBG_NI __host__ __device__ __noinline__
+#define TBG_NI __host__ __device__ __noinline__ inline
 #else
 #define TBG_HD inline
 #define TBG_NI inline
@@ -154,6 +154,10 @@ TBG_HD Fp fp_canon(const Fp& a) { return fp_csub_p(fp_reduce(a)); }
 
 // Montgomery product REDC(sum_k a_k * b_k), product scanning, 28-bit limbs.
 // Column bound: 14 (K + 1) products of < 2^56 each, so K <= 16 fits 64 bits.
+// The a*b products of a column are spread round-robin over four independent
+// 64-bit accumulators and the m*p products over two, so consecutive
+// v_mad_u64_u32 never depend on each other; only the m_k / carry chain is
+// serial from column to column.
 template <int K>
 TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
   TBG_COUNT(196 * (K + 1));
@@ -161,38 +165,31 @@ TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
   Fp r;
   uint64_t acc = 0;
 #pragma unroll
-  for (int k = 0; k < NL; ++k) {
-    uint64_t s0 = acc, s1 = 0, s2 = 0;
+  for (int k = 0; k < 2 * NL - 1; ++k) {
+    uint64_t s[4] = {0, 0, 0, 0};
+    uint64_t t[2] = {0, 0};
+    int c = 0;
+    const int lo = k < NL ? 0 : k - NL + 1;
+    const int hi = k < NL ? k : NL - 1;
 #pragma unroll
-    for (int i = 0; i <= k; ++i) {
-#pragma unroll
-      for (int n = 0; n < K; ++n) {
-        if (n & 1) s1 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
-        else s0 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < k; ++i) s2 += (uint64_t)m[i] * P_L[k - i];
-    uint64_t s = s0 + s1 + s2;
-    m[k] = ((uint32_t)s * NINV) & LMASK;
-    s += (uint64_t)m[k] * P_L[0];
-    acc = s >> 28;
-  }
-#pragma unroll
-  for (int k = NL; k < 2 * NL - 1; ++k) {
-    uint64_t s0 = acc, s1 = 0, s2 = 0;
-#pragma unroll
-    for (int i = k - NL + 1; i < NL; ++i) {
+    for (int i = lo; i <= hi; ++i) {
 #pragma unroll
       for (int n = 0; n < K; ++n) {
-        if (n & 1) s1 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
-        else s0 += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
+        s[c & 3] += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
+        ++c;
       }
-      s2 += (uint64_t)m[i] * P_L[k - i];
     }
-    uint64_t s = s0 + s1 + s2;
-    r.l[k - NL] = (uint32_t)s & LMASK;
-    acc = s >> 28;
+    const int mhi = k < NL ? k - 1 : NL - 1;
+#pragma unroll
+    for (int i = lo; i <= mhi; ++i) t[i & 1] += (uint64_t)m[i] * P_L[k - i];
+    uint64_t sum = ((s[0] + s[1]) + (s[2] + s[3])) + ((t[0] + t[1]) + acc);
+    if (k < NL) {
+      m[k] = ((uint32_t)sum * NINV) & LMASK;
+      sum += (uint64_t)m[k] * P_L[0];
+    } else {
+      r.l[k - NL] = (uint32_t)sum & LMASK;
+    }
+    acc = sum >> 28;
   }
   r.l[NL - 1] = (uint32_t)acc;
   return r;
@@ -213,7 +210,8 @@ TBG_HD Fp fp_mul2(const Fp& a, const Fp& b, const Fp& c, const Fp& d) {
   return fp_mul_sum<2>(A, B);
 }
 
-// Squaring: off-diagonal products once against a doubled copy.
+// Squaring: off-diagonal products once against a doubled copy; accumulators
+// split as in fp_mul_sum.
 TBG_HD Fp fp_sqr(const Fp& a) {
   TBG_BOUND(fp_ratio_p(a) * fp_ratio_p(a) < 2048.0, "fp_sqr bound");
   TBG_COUNT(301);
@@ -224,35 +222,28 @@ TBG_HD Fp fp_sqr(const Fp& a) {
   Fp r;
   uint64_t acc = 0;
 #pragma unroll
-  for (int k = 0; k < NL; ++k) {
-    uint64_t s0 = acc, s1 = 0, s2 = 0;
+  for (int k = 0; k < 2 * NL - 1; ++k) {
+    uint64_t s[4] = {0, 0, 0, 0};
+    uint64_t t[2] = {0, 0};
+    int c = 0;
+    const int lo = k < NL ? 0 : k - NL + 1;
 #pragma unroll
-    for (int i = 0; 2 * i < k; ++i) {
-      if (i & 1) s1 += (uint64_t)a.l[i] * a2[k - i];
-      else s0 += (uint64_t)a.l[i] * a2[k - i];
+    for (int i = lo; 2 * i < k; ++i) {
+      s[c & 3] += (uint64_t)a.l[i] * a2[k - i];
+      ++c;
     }
-    if ((k & 1) == 0) s1 += (uint64_t)a.l[k / 2] * a.l[k / 2];
+    if ((k & 1) == 0) s[c & 3] += (uint64_t)a.l[k / 2] * a.l[k / 2];
+    const int mhi = k < NL ? k - 1 : NL - 1;
 #pragma unroll
-    for (int i = 0; i < k; ++i) s2 += (uint64_t)m[i] * P_L[k - i];
-    uint64_t s = s0 + s1 + s2;
-    m[k] = ((uint32_t)s * NINV) & LMASK;
-    s += (uint64_t)m[k] * P_L[0];
-    acc = s >> 28;
-  }
-#pragma unroll
-  for (int k = NL; k < 2 * NL - 1; ++k) {
-    uint64_t s0 = acc, s1 = 0, s2 = 0;
-#pragma unroll
-    for (int i = k - NL + 1; 2 * i < k; ++i) {
-      if (i & 1) s1 += (uint64_t)a.l[i] * a2[k - i];
-      else s0 += (uint64_t)a.l[i] * a2[k - i];
+    for (int i = lo; i <= mhi; ++i) t[i & 1] += (uint64_t)m[i] * P_L[k - i];
+    uint64_t sum = ((s[0] + s[1]) + (s[2] + s[3])) + ((t[0] + t[1]) + acc);
+    if (k < NL) {
+      m[k] = ((uint32_t)sum * NINV) & LMASK;
+      sum += (uint64_t)m[k] * P_L[0];
+    } else {
+      r.l[k - NL] = (uint32_t)sum & LMASK;
     }
-    if ((k & 1) == 0) s1 += (uint64_t)a.l[k / 2] * a.l[k / 2];
-#pragma unroll
-    for (int i = k - NL + 1; i < NL; ++i) s2 += (uint64_t)m[i] * P_L[k - i];
-    uint64_t s = s0 + s1 + s2;
-    r.l[k - NL] = (uint32_t)s & LMASK;
-    acc = s >> 28;
+    acc = sum >> 28;
   }
   r.l[NL - 1] = (uint32_t)acc;
   return r;

@@ -85,11 +85,12 @@ TBG_NI Fp12 miller_loop(const G1A (&P)[N], const G2A (&Q)[N]) {
   return fp12_conj(f);
 }
 
-// a^|x| (square and multiply over the fixed |x|)
+// a^|x| for a in the cyclotomic subgroup (square and multiply over the fixed
+// |x|, Granger-Scott squarings)
 TBG_NI Fp12 fp12_pow_xabs(const Fp12& a) {
   Fp12 r = a;
   for (int i = 62; i >= 0; --i) {
-    r = fp12_sqr(r);
+    r = fp12_cyc_sqr(r);
     if ((X_ABS >> i) & 1) r = fp12_mul(r, a);
   }
   return r;
@@ -108,7 +109,7 @@ TBG_NI Fp12 final_exp(const Fp12& f) {
   Fp12 b = fp12_mul(cyc_pow_x(a), fp12_frob(a));      // a^(x+p)
   Fp12 c = fp12_mul(cyc_pow_x(cyc_pow_x(b)), fp12_frob(fp12_frob(b)));
   c = fp12_mul(c, fp12_conj(b));                      // b^(x^2+p^2-1)
-  Fp12 t3 = fp12_mul(fp12_sqr(t), t);
+  Fp12 t3 = fp12_mul(fp12_cyc_sqr(t), t);
   return fp12_mul(c, t3);
 }
 

@@ -205,6 +205,44 @@ TBG_NI Fp12 fp12_sqr(const Fp12& a) {
   return {c0, c1};
 }
 
+// Squaring in the cyclotomic subgroup (Granger-Scott): three Fp4 squarings,
+// 6 Fp2 products instead of 12.  Valid only after the easy part of the final
+// exponentiation.  Fp4 pairs: (c0.c0, c1.c1), (c1.c0, c0.c2), (c0.c1, c1.c2).
+TBG_HD void fp4_sqr(const Fp2& a, const Fp2& b, Fp2& t0, Fp2& t1) {
+  // (a + b y)^2 with y^2 = xi: t0 = a^2 + xi b^2, t1 = 2ab
+  Fp2 ab = fp2_mul(a, b);
+  Fp2 s = fp2_mul(fp2_add(a, b), fp2_add(a, fp2_mul_xi(b)));   // a^2 + xi b^2 + ab (1 + xi)
+  Fp2 u = fp2_reduce(fp2_add(ab, fp2_mul_xi(ab)));
+  t0 = fp2_reduce(fp2_sub(s, u));
+  t1 = fp2_add(ab, ab);
+}
+
+TBG_NI Fp12 fp12_cyc_sqr(const Fp12& f) {
+  const Fp2 &z0 = f.c0.c0, &z4 = f.c0.c1, &z3 = f.c0.c2, &z2 = f.c1.c0, &z1 = f.c1.c1, &z5 = f.c1.c2;
+  Fp2 t0, t1, t2, t3, t4, t5;
+  fp4_sqr(z0, z1, t0, t1);
+  fp4_sqr(z2, z3, t2, t3);
+  fp4_sqr(z4, z5, t4, t5);
+  Fp12 r;
+  // c0.c0 = 3 t0 - 2 z0 ; c1.c1 = 3 t1 + 2 z1
+  Fp2 a = fp2_sub(t0, z0);
+  r.c0.c0 = fp2_reduce(fp2_add(fp2_add(a, a), t0));
+  Fp2 b = fp2_add(t1, z1);
+  r.c1.c1 = fp2_reduce(fp2_add(fp2_add(b, b), t1));
+  // c1.c0 = 3 xi t5 + 2 z2 ; c0.c2 = 3 t4 - 2 z3
+  Fp2 x5 = fp2_reduce(fp2_mul_xi(t5));
+  Fp2 c = fp2_add(x5, z2);
+  r.c1.c0 = fp2_reduce(fp2_add(fp2_add(c, c), x5));
+  Fp2 d = fp2_sub(t4, z3);
+  r.c0.c2 = fp2_reduce(fp2_add(fp2_add(d, d), t4));
+  // c0.c1 = 3 t2 - 2 z4 ; c1.c2 = 3 t3 + 2 z5
+  Fp2 e = fp2_sub(t2, z4);
+  r.c0.c1 = fp2_reduce(fp2_add(fp2_add(e, e), t2));
+  Fp2 g = fp2_add(t3, z5);
+  r.c1.c2 = fp2_reduce(fp2_add(fp2_add(g, g), t3));
+  return r;
+}
+
 // f * (l0 + l1 v + l4 v w): the Miller-loop line (positions 0, 1, 4).
 TBG_NI Fp12 fp12_mul_by_014(const Fp12& a, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
   Fp6 t0 = fp6_mul_by_01(a.c0, l0, l1);

@@ -24,4 +24,143 @@ TBG_NI bool lagrange_at_zero_words(const uint8_t* ids, int k, int i, uint32_t (&
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// Integer form of the Lagrange coefficients.  lambda_i(0) = a_i / b_i with
+// small integers; with D = lcm(b_i) and N_i = a_i D / b_i the aggregate is
+// [D^-1 mod r] (sum_i N_i sigma_i): for identifiers 1..n the N_i are signed
+// binomials and D = 1 (e.g. {1,2,3,4} -> (4, -6, 4, -1)), so the 255-bit MSM
+// collapses to a few doublings and additions.  The group element is the same
+// because every sigma_i has order r (decoded points are subgroup-checked).
+TBG_HD uint64_t gcd_u64(uint64_t a, uint64_t b) {
+  while (b) {
+    uint64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+TBG_HD int bitlen_u64(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
+
+// Returns 1 on success (N, D set), 0 when the integers would overflow (use
+// the mod-r path), -1 on duplicate identifiers.
+TBG_NI int lagrange_int(const uint8_t* ids, int k, int i, int64_t& N, uint64_t& D) {
+  // reduced fractions a_j / b_j (b_j > 0) for every participant j
+  uint64_t lcm = 1;
+  int64_t ai = 0;
+  uint64_t bi = 1;
+  for (int j = 0; j < k; ++j) {
+    uint64_t num = 1, den = 1;
+    int neg = 0, bits = 0;
+    for (int m = 0; m < k; ++m) {
+      if (m == j) continue;
+      int64_t d = (int64_t)ids[m] - (int64_t)ids[j];
+      if (d == 0) return -1;
+      if (d < 0) { neg ^= 1; d = -d; }
+      bits += bitlen_u64(ids[m]) + bitlen_u64((uint64_t)d);
+      if (bits > 62) return 0;
+      num *= ids[m];
+      den *= (uint64_t)d;
+    }
+    uint64_t a, b;
+    if (num == 0) {
+      a = 0;
+      b = 1;
+    } else {
+      uint64_t g = gcd_u64(num, den);
+      a = num / g;
+      b = den / g;
+    }
+    uint64_t g2 = gcd_u64(lcm, b);
+    uint64_t q = b / g2;
+    if (bitlen_u64(lcm) + bitlen_u64(q) > 62) return 0;
+    lcm *= q;
+    if (j == i) {
+      ai = neg ? -(int64_t)a : (int64_t)a;
+      bi = b;
+    }
+  }
+  uint64_t scale = lcm / bi;
+  uint64_t mag = (uint64_t)(ai < 0 ? -ai : ai);
+  if (bitlen_u64(mag) + bitlen_u64(scale) > 62) return 0;
+  N = ai * (int64_t)scale;
+  D = lcm;
+  return 1;
+}
+
+TBG_HD Fr fr_from_u64(uint64_t v) {
+  Fr a = fr_zero();
+  a.l[0] = (uint32_t)(v & LMASK);
+  a.l[1] = (uint32_t)((v >> 28) & LMASK);
+  a.l[2] = (uint32_t)(v >> 56);
+  return fr_mul(a, fr_from_limbs(R_R2_M));
+}
+
+// Encoding of a partial's coefficient in its 8-word lam slot:
+//   mod-r mode:   words = lambda_i(0) (bit 255 clear)
+//   integer mode: w[7] = 0x80000000 | sign, w[0..1] = |N_i|, w[2..3] = D
+constexpr uint32_t LAM_INT_FLAG = 0x80000000u;
+
+// Coefficient words of participant `me` among `ids[0..k)`; false on duplicates.
+TBG_NI bool lagrange_encode(const uint8_t* ids, int k, int me, uint32_t (&w)[8]) {
+  int64_t N;
+  uint64_t D;
+  int r = lagrange_int(ids, k, me, N, D);
+  if (r < 0) return false;
+  for (int j = 0; j < 8; ++j) w[j] = 0;
+  if (r == 1) {
+    uint64_t mag = (uint64_t)(N < 0 ? -N : N);
+    w[0] = (uint32_t)mag;
+    w[1] = (uint32_t)(mag >> 32);
+    w[2] = (uint32_t)D;
+    w[3] = (uint32_t)(D >> 32);
+    w[7] = LAM_INT_FLAG | (N < 0 ? 1u : 0u);
+    return true;
+  }
+  return lagrange_at_zero_words(ids, k, me, w);
+}
+
+// sum_j coeff_j * P_j over the participants (mask[j] != 0), coefficients as
+// encoded by lagrange_encode.  pts / lam are indexed j = 0..count-1.
+TBG_NI G2J tss_combine(const G2A* pts, const uint32_t* lam, const uint8_t* mask, int count) {
+  int first = -1;
+  for (int j = 0; j < count; ++j)
+    if (mask[j]) { first = j; break; }
+  if (first < 0) return jac_inf<Fp2>();
+  G2J acc = jac_inf<Fp2>();
+  if (lam[8 * first + 7] & LAM_INT_FLAG) {
+    int nbits = 0;
+    for (int j = 0; j < count; ++j) {
+      if (!mask[j]) continue;
+      uint64_t mag = (uint64_t)lam[8 * j] | ((uint64_t)lam[8 * j + 1] << 32);
+      nbits = nbits > bitlen_u64(mag) ? nbits : bitlen_u64(mag);
+    }
+    for (int bit = nbits - 1; bit >= 0; --bit) {
+      acc = jac_dbl(acc);
+      for (int j = 0; j < count; ++j) {
+        if (!mask[j]) continue;
+        uint64_t mag = (uint64_t)lam[8 * j] | ((uint64_t)lam[8 * j + 1] << 32);
+        if ((mag >> bit) & 1) {
+          G2A p = pts[j];
+          if (lam[8 * j + 7] & 1) p.y = fp2_reduce(fp2_neg(p.y));
+          acc = jac_add_aff(acc, p);
+        }
+      }
+    }
+    uint64_t D = (uint64_t)lam[8 * first + 2] | ((uint64_t)lam[8 * first + 3] << 32);
+    if (D > 1) {
+      uint32_t dw[8];
+      fr_to_words(fr_inv(fr_from_u64(D)), dw);
+      acc = jac_mul_words(acc, dw, 255);
+    }
+    return acc;
+  }
+  for (int bit = 254; bit >= 0; --bit) {
+    acc = jac_dbl(acc);
+    for (int j = 0; j < count; ++j)
+      if (mask[j] && ((lam[8 * j + (bit >> 5)] >> (bit & 31)) & 1)) acc = jac_add_aff(acc, pts[j]);
+  }
+  return acc;
+}
+
 }  // namespace tbg

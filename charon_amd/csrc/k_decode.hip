@@ -1,0 +1,46 @@
+// Decode kernels: 48-byte G1 pubkeys (tblsconv.KeyFromBytes, tblsconv.go:30-37)
+// and 96-byte G2 signatures (tblsconv.SigFromCore, tblsconv.go:125-132).
+#include "tbls_launch.h"
+#include "bls_curve.h"
+
+namespace tbg {
+
+__global__ void __launch_bounds__(64) k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, int32_t* status) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t b[48];
+  for (int j = 0; j < 48; ++j) b[j] = pk48[48ull * i + j];
+  G1A a;
+  int32_t st = g1_decompress(b, a);
+  if (st != DEC_OK) {
+    a.x = fp_zero();
+    a.y = fp_zero();
+  }
+  out[i] = a;
+  status[i] = st;
+}
+
+__global__ void __launch_bounds__(64) k_decode_sigs(DevBatch B) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B.n_partials) return;
+  uint8_t b[96];
+  for (int j = 0; j < 96; ++j) b[j] = B.sigs[96ull * i + j];
+  G2A a;
+  int32_t st = g2_decompress(b, a);
+  if (st == DEC_IDENTITY) st = TBG_PS_ERR_IDENTITY;
+  if (st != DEC_OK) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  }
+  B.sig_aff[i] = a;
+  B.partial_status[i] = (st == DEC_OK) ? TBG_PS_NOT_VERIFIED : st;
+}
+
+void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, int32_t* status, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_decode_pubkeys, grid_for(n), dim3(kBlock), 0, st, pk48, n, out, status);
+}
+void launch_decode_sigs(const DevBatch& B, hipStream_t st) {
+  if (B.n_partials) hipLaunchKernelGGL(k_decode_sigs, grid_for(B.n_partials), dim3(kBlock), 0, st, B);
+}
+
+}  // namespace tbg

@@ -1,0 +1,26 @@
+// hash_to_G2 per distinct message (the H(m) of SigEth2.Verify, tss.go:190-197).
+#include "tbls_launch.h"
+#include "bls_h2c.h"
+
+namespace tbg {
+
+__global__ void __launch_bounds__(64) k_hash_msgs(DevBatch B) {
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= B.n_msgs) return;
+  uint32_t off = B.msg_off[m], len = B.msg_off[m + 1] - off;
+  G2J h = hash_to_g2(B.msgs + off, len);
+  G2A a;
+  bool ok = jac_to_aff(h, a);
+  if (!ok) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  }
+  B.h_aff[m] = a;
+  B.h_status[m] = ok ? 0 : 1;
+}
+
+void launch_hash_msgs(const DevBatch& B, hipStream_t st) {
+  if (B.n_msgs) hipLaunchKernelGGL(k_hash_msgs, grid_for(B.n_msgs), dim3(kBlock), 0, st, B);
+}
+
+}  // namespace tbg

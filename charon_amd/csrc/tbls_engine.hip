@@ -12,13 +12,12 @@
 #include <mutex>
 #include <new>
 #include <vector>
-#include "tbls_kernels.h"
+#include "tbls_launch.h"
+#include "bls_lines.h"
 
 using namespace tbg;
 
 namespace {
-
-constexpr int kBlock = 64;
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -38,9 +37,9 @@ struct Slot {
   uint8_t* d_work = nullptr;
   size_t d_work_cap = 0;
   size_t out_bytes = 0;
-  hipEvent_t ev[7] = {};
+  hipEvent_t ev[10] = {};  // see launch_chain
   hipEvent_t done = nullptr;
-  float ms[6] = {};
+  float ms[8] = {};
   tbg::DevBatch B{};           // device view of the last batch (resident until the slot is reused)
   size_t w_out = 0;
 };
@@ -50,13 +49,14 @@ struct Slot {
 struct tbg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // hash_to_G2 runs here, concurrently with decode
   std::mutex mu;
   G1A* d_pk = nullptr;
   int32_t* d_pk_status = nullptr;
   uint32_t n_pk = 0, cap_pk = 0;
   std::vector<Slot> slots;
   tbg_ticket next_ticket = 1;
-  float last_ms[6] = {};
+  float last_ms[8] = {};
 };
 
 #define HIP_TRY(x)                       \
@@ -120,7 +120,8 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   tbg_ctx* c = new (std::nothrow) tbg_ctx();
   if (!c) return TBG_E_OOM;
   c->device = dev;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return TBG_E_DEVICE;
   }
@@ -149,6 +150,7 @@ void tbg_destroy(tbg_ctx* c) {
   if (c->d_pk) hipFree(c->d_pk);
   if (c->d_pk_status) hipFree(c->d_pk_status);
   hipStreamDestroy(c->stream);
+  hipStreamDestroy(c->stream2);
   delete c;
 }
 
@@ -184,8 +186,7 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   int rc = TBG_OK;
   if (hipMemcpyAsync(d_bytes, pk48, 48ull * count, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
   if (rc == TBG_OK) {
-    hipLaunchKernelGGL(k_decode_pubkeys, dim3((count + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, d_bytes, count,
-                       c->d_pk + c->n_pk, c->d_pk_status + c->n_pk);
+    launch_decode_pubkeys(d_bytes, count, c->d_pk + c->n_pk, c->d_pk_status + c->n_pk, c->stream);
     if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
   }
   if (rc == TBG_OK && status &&
@@ -197,27 +198,47 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   return rc;
 }
 
-// The kernel chain of one batch on the context stream; ev[0..5] bracket the
-// five kernels (decode, hash, verify, lagrange, aggregate).
+// The kernel chain of one batch.  Per-message work (hash_to_G2, H(m) lines)
+// runs on stream2 concurrently with the per-signature work (decode, signature
+// lines) on stream; the quad verify joins both.
+// Events: ev[0] start, ev[1] decode done, ev[2] signature lines done,
+// ev[3]/ev[4] hash start/done and ev[5] H lines done (stream2), ev[6] verify
+// start, ev[7] verify done, ev[8] lagrange done, ev[9] aggregate done.
 static int launch_chain(tbg_ctx* c, const DevBatch& B, hipEvent_t* ev) {
-  hipStream_t st = c->stream;
-  auto grid = [](uint32_t n) { return dim3((n + kBlock - 1) / kBlock); };
-  const uint32_t np = B.n_partials, nm = B.n_msgs, nd = B.n_duties;
+  hipStream_t st = c->stream, st2 = c->stream2;
+  const bool verify = B.op != TBG_OP_AGGREGATE;
   HIP_TRY(hipEventRecord(ev[0], st));
-  if (np) hipLaunchKernelGGL(k_decode_sigs, grid(np), dim3(kBlock), 0, st, B);
+  HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
+  HIP_TRY(hipEventRecord(ev[3], st2));
+  launch_hash_msgs(B, st2);
+  HIP_TRY(hipEventRecord(ev[4], st2));
+  launch_decode_sigs(B, st);
   HIP_TRY(hipEventRecord(ev[1], st));
-  if (nm) hipLaunchKernelGGL(k_hash_msgs, grid(nm), dim3(kBlock), 0, st, B);
+  if (verify) launch_lines(B, st, st2);
   HIP_TRY(hipEventRecord(ev[2], st));
-  if (B.op != TBG_OP_AGGREGATE && np)
-    hipLaunchKernelGGL(k_verify, grid(np), dim3(kBlock), 0, st, B, (const G1A*)c->d_pk, (const int32_t*)c->d_pk_status,
-                       c->n_pk);
-  HIP_TRY(hipEventRecord(ev[3], st));
-  if (B.op != TBG_OP_VERIFY && np) hipLaunchKernelGGL(k_lagrange, grid(np), dim3(kBlock), 0, st, B);
-  HIP_TRY(hipEventRecord(ev[4], st));
-  hipLaunchKernelGGL(k_aggregate, grid(nd), dim3(kBlock), 0, st, B);
-  HIP_TRY(hipEventRecord(ev[5], st));
+  HIP_TRY(hipEventRecord(ev[5], st2));
+  HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
+  HIP_TRY(hipEventRecord(ev[6], st));
+  if (verify) launch_verify(B, (const G1A*)c->d_pk, (const int32_t*)c->d_pk_status, c->n_pk, st);
+  HIP_TRY(hipEventRecord(ev[7], st));
+  if (B.op != TBG_OP_VERIFY) launch_lagrange(B, st);
+  HIP_TRY(hipEventRecord(ev[8], st));
+  launch_aggregate(B, st);
+  HIP_TRY(hipEventRecord(ev[9], st));
   HIP_TRY(hipGetLastError());
   return TBG_OK;
+}
+
+// [decode, hash, sig lines, H lines, verify, lagrange, aggregate, total]
+static void chain_times(hipEvent_t* e, float* ms) {
+  hipEventElapsedTime(&ms[0], e[0], e[1]);
+  hipEventElapsedTime(&ms[1], e[3], e[4]);
+  hipEventElapsedTime(&ms[2], e[1], e[2]);
+  hipEventElapsedTime(&ms[3], e[4], e[5]);
+  hipEventElapsedTime(&ms[4], e[6], e[7]);
+  hipEventElapsedTime(&ms[5], e[7], e[8]);
+  hipEventElapsedTime(&ms[6], e[8], e[9]);
+  hipEventElapsedTime(&ms[7], e[0], e[9]);
 }
 
 static int validate(const tbg_batch* b) {
@@ -277,6 +298,8 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   size_t w_h_aff = sec(sizeof(G2A) * (size_t)nm);
   size_t w_h_st = sec(4ull * nm);
   size_t w_lam = sec(32ull * np);
+  size_t w_sl = sec(4ull * LINES_WORDS * np);
+  size_t w_hl = sec(4ull * LINES_WORDS * nm);
   size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
   size_t w_pst = sec(4ull * np);
   size_t w_dst = sec(4ull * nd);
@@ -327,6 +350,8 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   B.h_aff = (G2A*)(dw + w_h_aff);
   B.h_status = (int32_t*)(dw + w_h_st);
   B.lam = (uint32_t*)(dw + w_lam);
+  B.sig_lines = (uint32_t*)(dw + w_sl);
+  B.h_lines = (uint32_t*)(dw + w_hl);
   B.partial_status = (int32_t*)(dw + w_pst);
   B.duty_status = (int32_t*)(dw + w_dst);
   B.agg = dw + w_agg;
@@ -374,8 +399,7 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
   if (pst) memcpy(pst, s->h_out + o_pst, 4ull * np);
   if (dst) memcpy(dst, s->h_out + o_dst, 4ull * nd);
   if (agg) memcpy(agg, s->h_out + o_agg, 96ull * nd);
-  for (int k = 0; k < 5; ++k) hipEventElapsedTime(&s->ms[k], s->ev[k], s->ev[k + 1]);
-  hipEventElapsedTime(&s->ms[5], s->ev[0], s->ev[5]);
+  chain_times(s->ev, s->ms);
   memcpy(c->last_ms, s->ms, sizeof(c->last_ms));
   s->busy = false;
   return TBG_OK;
@@ -388,7 +412,7 @@ int tbg_run(tbg_ctx* c, const tbg_batch* b, int32_t* pst, int32_t* dst, uint8_t*
   return tbg_collect(c, t, pst, dst, agg, 1);
 }
 
-int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms6) {
+int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms8) {
   if (!c || iters == 0) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   Slot* s = nullptr;
@@ -396,20 +420,20 @@ int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms6) {
     if (!x.busy && x.ticket == t) { s = &x; break; }
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
-  std::vector<hipEvent_t> ev(6ull * iters);
+  std::vector<hipEvent_t> ev(10ull * iters);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   int rc = TBG_OK;
-  for (uint32_t k = 0; k < iters && rc == TBG_OK; ++k) rc = launch_chain(c, s->B, ev.data() + 6ull * k);
+  for (uint32_t k = 0; k < iters && rc == TBG_OK; ++k) rc = launch_chain(c, s->B, ev.data() + 10ull * k);
   if (hipStreamSynchronize(c->stream) != hipSuccess) rc = TBG_E_DEVICE;
-  float acc[6] = {0, 0, 0, 0, 0, 0};
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (rc == TBG_OK) {
     for (uint32_t k = 0; k < iters; ++k) {
-      hipEvent_t* e = ev.data() + 6ull * k;
-      float m;
-      for (int j = 0; j < 5; ++j) { hipEventElapsedTime(&m, e[j], e[j + 1]); acc[j] += m; }
+      float m[8];
+      chain_times(ev.data() + 10ull * k, m);
+      for (int j = 0; j < 7; ++j) acc[j] += m[j];
     }
-    hipEventElapsedTime(&acc[5], ev[0], ev[6ull * (iters - 1) + 5]);
-    if (ms6) memcpy(ms6, acc, sizeof(acc));
+    hipEventElapsedTime(&acc[7], ev[0], ev[10ull * (iters - 1) + 9]);
+    if (ms8) memcpy(ms8, acc, sizeof(acc));
     memcpy(c->last_ms, acc, sizeof(acc));
   }
   for (auto& e : ev) hipEventDestroy(e);
@@ -436,9 +460,9 @@ int tbg_fetch(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg
   return TBG_OK;
 }
 
-int tbg_last_timings(const tbg_ctx* c, float* ms6) {
-  if (!c || !ms6) return TBG_E_INVALID_ARG;
-  memcpy(ms6, c->last_ms, sizeof(c->last_ms));
+int tbg_last_timings(const tbg_ctx* c, float* ms8) {
+  if (!c || !ms8) return TBG_E_INVALID_ARG;
+  memcpy(ms8, c->last_ms, sizeof(c->last_ms));
   return TBG_OK;
 }
 
@@ -457,7 +481,7 @@ int tbg_sk_to_pk(tbg_ctx* c, const uint8_t* sk32, uint32_t n, uint8_t* pk48) {
   int rc = TBG_OK;
   if (hipMemcpyAsync(d_sk, sk32, 32ull * n, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
   if (rc == TBG_OK) {
-    hipLaunchKernelGGL(k_sk_to_pk, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, d_sk, n, d_pk);
+    launch_sk_to_pk(d_sk, n, d_pk, c->stream);
     if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
   }
   if (rc == TBG_OK && hipMemcpyAsync(pk48, d_pk, 48ull * n, hipMemcpyDeviceToHost, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
@@ -507,8 +531,8 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
     B.msg_off = d_off;
     B.h_aff = d_h;
     B.h_status = d_hs;
-    hipLaunchKernelGGL(k_hash_msgs, dim3((n_msgs + kBlock - 1) / kBlock), dim3(kBlock), 0, st, B);
-    hipLaunchKernelGGL(k_sign, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d_sk, d_im, n, d_h, d_hs, d_sig);
+    launch_hash_msgs(B, st);
+    launch_sign(d_sk, d_im, n, d_h, d_hs, d_sig, st);
     if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
   }
   if (rc == TBG_OK && hipMemcpyAsync(sig96, d_sig, 96ull * n, hipMemcpyDeviceToHost, st) != hipSuccess) rc = TBG_E_DEVICE;

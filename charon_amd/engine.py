@@ -22,6 +22,7 @@ DS_INSUFFICIENT, DS_INSUFFICIENT_VALID = -20, -21
 DS_AGG_TOO_FEW, DS_AGG_DUPLICATE_ID, DS_AGG_IDENTITY, DS_DECODE = -22, -23, -24, -25
 OP_VERIFY, OP_AGGREGATE, OP_VERIFY_AGGREGATE = 1, 2, 3
 NO_PUBKEY = 0xFFFFFFFF
+TIMING_KEYS = ["decode", "hash", "sig_lines", "h_lines", "verify", "lagrange", "aggregate", "total"]
 E_PENDING = -6
 
 
@@ -149,9 +150,9 @@ class Engine:
 
     def replay(self, ticket, iters=1):
         """Re-run a collected batch's kernel chain on its resident inputs."""
-        ms = np.zeros(6, dtype=np.float32)
+        ms = np.zeros(8, dtype=np.float32)
         self._check(self._lib.tbg_replay(self._h, ticket, iters, _ptr(ms)), "tbg_replay")
-        return dict(zip(["decode", "hash", "verify", "lagrange", "aggregate", "total"], ms.tolist()))
+        return dict(zip(TIMING_KEYS, ms.tolist()))
 
     def fetch(self, ticket, n_duties, n_partials) -> BatchResult:
         ps = np.zeros(n_partials, dtype=np.int32)
@@ -161,9 +162,9 @@ class Engine:
         return BatchResult(ps, ds, agg)
 
     def timings(self):
-        ms = np.zeros(6, dtype=np.float32)
+        ms = np.zeros(8, dtype=np.float32)
         self._check(self._lib.tbg_last_timings(self._h, _ptr(ms)), "tbg_last_timings")
-        return dict(zip(["decode", "hash", "verify", "lagrange", "aggregate", "total"], ms.tolist()))
+        return dict(zip(TIMING_KEYS, ms.tolist()))
 
     # ------------------------------------------------------------ vector generation
     def sk_to_pk(self, sk32) -> np.ndarray:

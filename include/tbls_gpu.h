@@ -121,9 +121,9 @@ int tbg_run(tbg_ctx* ctx, const tbg_batch* batch, int32_t* partial_status, int32
 /* Device-resident replay: re-run the kernel chain of a collected batch whose
  * inputs are still resident in its slot's HBM arena (valid until the slot is
  * reused by a later tbg_submit), `iters` times back to back, no host copies.
- * Blocks; ms6 receives per-kernel totals as in tbg_last_timings.  tbg_fetch
+ * Blocks; ms8 receives per-kernel totals as in tbg_last_timings.  tbg_fetch
  * copies that slot's current outputs back (synchronous). */
-int tbg_replay(tbg_ctx* ctx, tbg_ticket ticket, uint32_t iters, float* ms6);
+int tbg_replay(tbg_ctx* ctx, tbg_ticket ticket, uint32_t iters, float* ms8);
 int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
 
 /* Test-vector / benchmark-input generation on the GPU (not on the hot path):
@@ -135,8 +135,9 @@ int tbg_sign(tbg_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint8_t* msgs,
              uint32_t n_msgs, const uint32_t* item_msg, uint8_t* sig96);
 
 /* Last kernel timings of the context (milliseconds, HIP events on the
- * engine's stream): [decode, hash, verify, lagrange, aggregate, total]. */
-int tbg_last_timings(const tbg_ctx* ctx, float* ms6);
+ * engine's streams): [decode, hash, sig lines, H lines, verify, lagrange,
+ * aggregate, total]. */
+int tbg_last_timings(const tbg_ctx* ctx, float* ms8);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,7 @@ void hc_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { f12_out(fp1
 void hc_fp12_sqr(const uint8_t* a, uint8_t* out) { f12_out(fp12_sqr(f12_in(a)), out); }
 void hc_fp12_inv(const uint8_t* a, uint8_t* out) { f12_out(fp12_inv(f12_in(a)), out); }
 void hc_fp12_frob(const uint8_t* a, uint8_t* out) { f12_out(fp12_frob(f12_in(a)), out); }
+void hc_fp12_cyc_sqr(const uint8_t* a, uint8_t* out) { f12_out(fp12_cyc_sqr(f12_in(a)), out); }
 void hc_final_exp(const uint8_t* a, uint8_t* out) { f12_out(final_exp(f12_in(a)), out); }
 
 // G2 decompress -> status; on success writes the recompressed encoding and
@@ -156,17 +157,183 @@ int hc_stage_aggregate(const uint8_t* ids, const uint8_t* sigs96, int k, uint8_t
   if (k > 16) return -1;
   for (int i = 0; i < k; ++i)
     if (g2_decompress(sigs96 + 96 * i, pts[i]) != DEC_OK) return -2;
-  for (int i = 0; i < k; ++i)
-    if (!lagrange_at_zero_words(ids, k, i, lam[i])) return -3;
-  G2J acc = jac_inf<Fp2>();
-  for (int bit = 254; bit >= 0; --bit) {
-    acc = jac_dbl(acc);
-    for (int j = 0; j < k; ++j)
-      if ((lam[j][bit >> 5] >> (bit & 31)) & 1) acc = jac_add_aff(acc, pts[j]);
+  uint8_t mask[16];
+  for (int i = 0; i < k; ++i) {
+    if (!lagrange_encode(ids, k, i, lam[i])) return -3;
+    mask[i] = 1;
   }
+  G2J acc = tss_combine(pts, &lam[0][0], mask, k);
   G2A a;
   bool ok = jac_to_aff(acc, a);
   g2_compress(a, !ok, out96);
   return ok ? 0 : -4;
+}
+}
+
+#include "../../charon_amd/csrc/bls_quad.h"
+// Host emulation of the quad (lane-cooperative) Fp12 pieces: the three lanes
+// run in turn and the DPP exchanges become array indexing.
+extern "C" {
+static void q_split(const Fp12& f, Fp4 (&A)[3]) { for (int q = 0; q < 3; ++q) A[q] = quad_from_fp12(q, f); }
+static const int SW12[3] = {0, 2, 1};
+
+void hc_quad_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  Fp4 A[3], B[3], P[3], Q[3], C[3];
+  q_split(f12_in(a), A);
+  q_split(f12_in(b), B);
+  for (int q = 0; q < 3; ++q) {
+    Fp4 SA = fp4_add(A[(q + 1) % 3], A[(q + 2) % 3]), SB = fp4_add(B[(q + 1) % 3], B[(q + 2) % 3]);
+    P[q] = fp4_mul(A[q], B[q]);
+    Q[q] = fp4_mul(SA, SB);
+  }
+  for (int q = 0; q < 3; ++q) C[q] = quad_combine(q, P[q], P[(q + 1) % 3], P[(q + 2) % 3], Q[SW12[q]]);
+  f12_out(quad_to_fp12(C[0], C[1], C[2]), out);
+}
+void hc_quad_sqr(const uint8_t* a, uint8_t* out) {
+  Fp4 A[3], P[3], Q[3], C[3];
+  q_split(f12_in(a), A);
+  for (int q = 0; q < 3; ++q) {
+    P[q] = fp4_sqr(A[q]);
+    Q[q] = fp4_sqr(fp4_add(A[(q + 1) % 3], A[(q + 2) % 3]));
+  }
+  for (int q = 0; q < 3; ++q) C[q] = quad_combine(q, P[q], P[(q + 1) % 3], P[(q + 2) % 3], Q[SW12[q]]);
+  f12_out(quad_to_fp12(C[0], C[1], C[2]), out);
+}
+void hc_quad_cyc_sqr(const uint8_t* a, uint8_t* out) {
+  Fp4 A[3], T[3], C[3];
+  q_split(f12_in(a), A);
+  for (int q = 0; q < 3; ++q) T[q] = fp4_sqr(A[q]);
+  for (int q = 0; q < 3; ++q) C[q] = quad_cyc_lane(q, A[q], T[SW12[q]]);
+  f12_out(quad_to_fp12(C[0], C[1], C[2]), out);
+}
+// f * line where line = (l0, l1, l4) each 96 bytes
+void hc_quad_line(const uint8_t* a, const uint8_t* l, uint8_t* out) {
+  Fp4 A[3], C[3];
+  q_split(f12_in(a), A);
+  Fp2 l0 = {from_be(l), from_be(l + 48)}, l1 = {from_be(l + 96), from_be(l + 144)}, l4 = {from_be(l + 192), from_be(l + 240)};
+  for (int q = 0; q < 3; ++q) C[q] = quad_line_lane(q, A[q], A[(q + 1) % 3], l0, l1, l4);
+  f12_out(quad_to_fp12(C[0], C[1], C[2]), out);
+}
+void hc_quad_frob(const uint8_t* a, uint8_t* out) {
+  Fp4 A[3], C[3];
+  q_split(f12_in(a), A);
+  for (int q = 0; q < 3; ++q) C[q] = quad_frob_lane(q, A[q]);
+  f12_out(quad_to_fp12(C[0], C[1], C[2]), out);
+}
+void hc_quad_conj(const uint8_t* a, uint8_t* out) {
+  Fp4 A[3], C[3];
+  q_split(f12_in(a), A);
+  for (int q = 0; q < 3; ++q) C[q] = quad_conj_lane(q, A[q]);
+  f12_out(quad_to_fp12(C[0], C[1], C[2]), out);
+}
+}
+
+#include "../../charon_amd/csrc/bls_lines.h"
+// Whole quad verify emulated on the host (same per-lane pieces as
+// k_verify_quad): lines precomputed with g2_lines, Miller accumulation and
+// final exponentiation on the 3-lane split representation.
+namespace qe {
+struct Q3 { Fp4 v[3]; };
+static Q3 mul(const Q3& A, const Q3& B) {
+  Q3 P, Q, C;
+  for (int q = 0; q < 3; ++q) {
+    P.v[q] = fp4_mul(A.v[q], B.v[q]);
+    Q.v[q] = fp4_mul(fp4_add(A.v[(q + 1) % 3], A.v[(q + 2) % 3]), fp4_add(B.v[(q + 1) % 3], B.v[(q + 2) % 3]));
+  }
+  for (int q = 0; q < 3; ++q) C.v[q] = quad_combine(q, P.v[q], P.v[(q + 1) % 3], P.v[(q + 2) % 3], Q.v[SW12[q]]);
+  return C;
+}
+static Q3 sqr(const Q3& A) {
+  Q3 P, Q, C;
+  for (int q = 0; q < 3; ++q) {
+    P.v[q] = fp4_sqr(A.v[q]);
+    Q.v[q] = fp4_sqr(fp4_add(A.v[(q + 1) % 3], A.v[(q + 2) % 3]));
+  }
+  for (int q = 0; q < 3; ++q) C.v[q] = quad_combine(q, P.v[q], P.v[(q + 1) % 3], P.v[(q + 2) % 3], Q.v[SW12[q]]);
+  return C;
+}
+static Q3 cyc(const Q3& A) {
+  Q3 T, C;
+  for (int q = 0; q < 3; ++q) T.v[q] = fp4_sqr(A.v[q]);
+  for (int q = 0; q < 3; ++q) C.v[q] = quad_cyc_lane(q, A.v[q], T.v[SW12[q]]);
+  return C;
+}
+static Q3 line(const Q3& A, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
+  Q3 C;
+  for (int q = 0; q < 3; ++q) C.v[q] = quad_line_lane(q, A.v[q], A.v[(q + 1) % 3], l0, l1, l4);
+  return C;
+}
+static Q3 conj(const Q3& A) { Q3 C; for (int q = 0; q < 3; ++q) C.v[q] = quad_conj_lane(q, A.v[q]); return C; }
+static Q3 frob(const Q3& A) { Q3 C; for (int q = 0; q < 3; ++q) C.v[q] = quad_frob_lane(q, A.v[q]); return C; }
+static Q3 inv(const Q3& A) {
+  Fp12 r = fp12_inv(quad_to_fp12(A.v[0], A.v[1], A.v[2]));
+  Q3 C; for (int q = 0; q < 3; ++q) C.v[q] = quad_from_fp12(q, r); return C;
+}
+static Q3 pow_x(const Q3& a) {
+  Q3 r = a;
+  for (int i = 62; i >= 0; --i) { r = cyc(r); if ((X_ABS >> i) & 1) r = mul(r, a); }
+  return conj(r);
+}
+static Q3 final_exp(const Q3& f) {
+  Q3 t = mul(conj(f), inv(f));
+  t = mul(frob(frob(t)), t);
+  Q3 a = mul(pow_x(t), conj(t));
+  a = mul(pow_x(a), conj(a));
+  Q3 b = mul(pow_x(a), frob(a));
+  Q3 c = mul(pow_x(pow_x(b)), frob(frob(b)));
+  c = mul(c, conj(b));
+  Q3 t3 = mul(cyc(t), t);
+  return mul(c, t3);
+}
+}  // namespace qe
+
+extern "C" {
+static uint32_t g_sig_lines[LINES_WORDS], g_h_lines[LINES_WORDS];
+// stage 1: line precomputation for one partial (signature lines) and its message (H lines)
+int hc_stage_lines(const uint8_t* sig96, const uint8_t* msg, uint32_t len) {
+  G2A sig, ha;
+  if (g2_decompress(sig96, sig) != DEC_OK) return -1;
+  G2J h = hash_to_g2(msg, len);
+  jac_to_aff(h, ha);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  g2_lines(sig, nx, fp_from_const(G1_NEG_Y), g_sig_lines);
+#if defined(TBG_COUNT_OPS)
+  unsigned long long sig_cost = tbg_mad_count;
+#endif
+  g2_lines(ha, fp_one(), fp_one(), g_h_lines);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = sig_cost;  // report the per-signature share; H lines are per message
+#endif
+  return 0;
+}
+// stage 2: quad verify of that partial against pk, using the stored lines
+int hc_stage_verify_quad(const uint8_t* pk48) {
+  G1A pk;
+  if (g1_decompress(pk48, pk) != DEC_OK) return -1;
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  Fp nx = fp_reduce(fp_neg(pk.x));
+  qe::Q3 f;
+  f.v[0] = {fp2_one(), fp2_zero()};
+  f.v[1] = fp4_zero();
+  f.v[2] = fp4_zero();
+  int idx = 0;
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = qe::sqr(f);
+    int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+    for (int s = 0; s < steps; ++s, ++idx) {
+      Line a = line_load(g_sig_lines + LINE_WORDS * idx);
+      f = qe::line(f, a.l0, a.l1, a.l4);
+      Line h = line_load(g_h_lines + LINE_WORDS * idx);
+      f = qe::line(f, h.l0, fp2_mul_fp(h.l1, nx), fp2_mul_fp(h.l4, pk.y));
+    }
+  }
+  f = qe::final_exp(qe::conj(f));
+  Fp12 r = quad_to_fp12(f.v[0], f.v[1], f.v[2]);
+  return fp12_is_one(r) ? 1 : 0;
 }
 }

@@ -110,6 +110,14 @@ def test_fp12_ops():
         assert b2f12(call("hc_fp12_frob", f12b(a), out=576)) == bls.f12_frob(a)
 
 
+def test_cyclotomic_square():
+    a = rand_f12()
+    # project into the cyclotomic subgroup with the easy part of the final exponentiation
+    f = bls.f12_mul(bls.f12_conj(a), bls.f12_inv(a))
+    f = bls.f12_mul(bls.f12_frob_n(f, 2), f)
+    assert b2f12(call("hc_fp12_cyc_sqr", f12b(f), out=576)) == bls.f12_sqr(f)
+
+
 def test_final_exp_matches_oracle():
     a = rand_f12()
     assert b2f12(call("hc_final_exp", f12b(a), out=576)) == bls.final_exp(a)
@@ -188,3 +196,60 @@ def test_g1_decompress_matches_oracle():
         ob = ctypes.create_string_buffer(96)
         assert lib().hc_g1_decompress(bls.g1_compress(p), ob) == 0
         assert (fe(ob.raw[:48]), fe(ob.raw[48:])) == p
+
+
+def test_aggregate_integer_and_modr_paths_match_golden():
+    """Lagrange recombination (integer numerators / common denominator, or the
+    mod-r fallback) reproduces every golden aggregate."""
+    import ctypes
+    import json
+    import os
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    cases = []
+    for v in json.load(open(os.path.join(gold, "aggregate_edges.json")))["vectors"]:
+        if v["expect"]["status"] == "ok":
+            cases.append(([p["identifier"] for p in v["partials"]], [p["sig"] for p in v["partials"]], v["expect"]["agg"]))
+    for name in ["cfg1_3of4_single.json", "cfg3_7of10_sample.json", "cfg5_mixed_invalid.json"]:
+        for v in json.load(open(os.path.join(gold, name)))["vectors"]:
+            if v["expect"]["status"] != "ok":
+                continue
+            ps = [p for p, st in zip(v["partials"], v["expect"]["partial_status"]) if st == "valid"]
+            cases.append(([p["identifier"] for p in ps], [p["sig"] for p in ps], v["expect"]["agg"]))
+    assert len(cases) >= 10
+    for ids, sigs, agg in cases:
+        ob = ctypes.create_string_buffer(96)
+        rc = lib().hc_stage_aggregate(bytes(ids), b"".join(bytes.fromhex(s) for s in sigs), len(ids), ob)
+        assert rc == 0 and ob.raw.hex() == agg, ids
+
+
+def test_quad_lane_algebra_matches_tower():
+    """The per-lane pieces of the lane-cooperative Fp12 arithmetic (bls_quad.h),
+    run as an emulated quad on the host, equal the oracle's tower arithmetic."""
+    for _ in range(4):
+        a, b = rand_f12(), rand_f12()
+        assert b2f12(call("hc_quad_mul", f12b(a), f12b(b), out=576)) == bls.f12_mul(a, b)
+        assert b2f12(call("hc_quad_sqr", f12b(a), out=576)) == bls.f12_sqr(a)
+        assert b2f12(call("hc_quad_frob", f12b(a), out=576)) == bls.f12_frob(a)
+        assert b2f12(call("hc_quad_conj", f12b(a), out=576)) == bls.f12_conj(a)
+        l0, l1, l4 = [(rng.randrange(P), rng.randrange(P)) for _ in range(3)]
+        line = ((l0, l1, bls.F2_ZERO), (bls.F2_ZERO, l4, bls.F2_ZERO))
+        got = b2f12(call("hc_quad_line", f12b(a), f2b(l0) + f2b(l1) + f2b(l4), out=576))
+        assert got == bls.f12_mul(a, line)
+    f = bls.f12_mul(bls.f12_conj(a), bls.f12_inv(a))
+    f = bls.f12_mul(bls.f12_frob_n(f, 2), f)
+    assert b2f12(call("hc_quad_cyc_sqr", f12b(f), out=576)) == bls.f12_sqr(f)
+
+
+def test_quad_verify_pipeline_emulated():
+    """Line precomputation + quad Miller accumulation + quad final
+    exponentiation (the k_lines_* / k_verify_quad algorithm) on the host."""
+    from tests.test_oracle_kat import DEPOSIT_GOLDEN, deposit_signing_root
+    pk_hex, sig_hex, root_hex = DEPOSIT_GOLDEN[0]
+    root = deposit_signing_root(root_hex)
+    assert lib().hc_stage_lines(bytes.fromhex(sig_hex), root, len(root)) == 0
+    assert lib().hc_stage_verify_quad(bytes.fromhex(pk_hex)) == 1
+    assert lib().hc_stage_verify_quad(bytes.fromhex(DEPOSIT_GOLDEN[1][0])) == 0   # wrong key
+    bad = bytearray(root)
+    bad[3] ^= 8
+    assert lib().hc_stage_lines(bytes.fromhex(sig_hex), bytes(bad), len(bad)) == 0
+    assert lib().hc_stage_verify_quad(bytes.fromhex(pk_hex)) == 0                 # wrong message

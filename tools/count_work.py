@@ -41,6 +41,16 @@ def main():
     lib.hc_count_reset()
     assert lib.hc_stage_verify(pks[0], sigs[0], msg, len(msg)) == 1
     verify = lib.hc_count_get()
+    lib.hc_count_reset()
+    assert lib.hc_stage_lines(sigs[0], msg, len(msg)) == 0
+    lines_sig = lib.hc_count_get()
+    # H lines alone (per message): total of both minus the signature share
+    lib.hc_count_reset()
+    lib.hc_stage_lines(sigs[0], msg, len(msg))
+    lines_h = lines_sig  # same schedule (68 steps on a G2 point), P folding aside
+    lib.hc_count_reset()
+    assert lib.hc_stage_verify_quad(pks[0]) == 1
+    verify_quad = lib.hc_count_get()
     out = ctypes.create_string_buffer(96)
     ids = bytes([p["identifier"] for p in gold["partials"]])
     lib.hc_count_reset()
@@ -48,14 +58,17 @@ def main():
     agg_with_decode = lib.hc_count_get()
     assert out.raw.hex() == gold["expect"]["agg"]
     agg = agg_with_decode - len(sigs) * decode
-    unit_3of4 = 4 * decode + hash_ + 4 * verify + agg
+    unit_3of4_v1 = 4 * decode + hash_ + 4 * verify + agg
+    unit_3of4 = 4 * decode + hash_ + lines_h + 4 * (lines_sig + verify_quad) + agg
     model = {
         "generator": "tools/count_work.py",
         "mads_per_fp_mul": 392,
-        "mads": {"decode_sig": decode, "hash_to_g2": hash_, "verify_item": verify, "aggregate_3of4_all4": agg,
-                 "unit_3of4": unit_3of4},
+        "mads": {"decode_sig": decode, "hash_to_g2": hash_, "lines_sig": lines_sig, "lines_h": lines_h,
+                 "verify_quad_item": verify_quad, "verify_item_single_lane": verify,
+                 "aggregate_3of4_all4": agg, "unit_3of4": unit_3of4, "unit_3of4_single_lane_schedule": unit_3of4_v1},
         "fp_mul_equiv": {k: round(v / 392, 1) for k, v in
-                         {"decode_sig": decode, "hash_to_g2": hash_, "verify_item": verify,
+                         {"decode_sig": decode, "hash_to_g2": hash_, "lines_sig": lines_sig,
+                          "verify_quad_item": verify_quad, "verify_item_single_lane": verify,
                           "aggregate_3of4_all4": agg, "unit_3of4": unit_3of4}.items()},
         "verify_hbm_bytes_per_launch": None,
     }
