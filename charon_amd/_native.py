@@ -49,7 +49,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     units = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
     objdir = os.path.join(PKG, "build_obj", os.path.basename(target).replace(".so", ""))
     os.makedirs(objdir, exist_ok=True)
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed", "-Wno-unused-result"]
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed", "-Wno-unused-result", "-Wno-unused-value"]
     flags += ["-D" + d for d in defines]
 
     def compile_unit(u):
@@ -113,6 +113,8 @@ SIGNATURES = {
     "tbg_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TbgBatch), ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p]),
     "tbg_replay": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
+    "tbg_replay_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p]),
     "tbg_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_last_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_sk_to_pk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),

@@ -37,6 +37,8 @@ struct Slot {
   uint8_t* d_work = nullptr;
   size_t d_work_cap = 0;
   size_t out_bytes = 0;
+  hipStream_t st = nullptr;   // per-signature chain (decode, lines, verify, aggregate)
+  hipStream_t st2 = nullptr;  // per-message chain (hash_to_G2, H(m) lines), joins st before verify
   hipEvent_t ev[10] = {};  // see launch_chain
   hipEvent_t done = nullptr;
   float ms[8] = {};
@@ -48,8 +50,7 @@ struct Slot {
 
 struct tbg_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // hash_to_G2 runs here, concurrently with decode
+  hipStream_t stream = nullptr;  // utility stream (pubkey table, test-vector generation)
   std::mutex mu;
   G1A* d_pk = nullptr;
   int32_t* d_pk_status = nullptr;
@@ -120,14 +121,21 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   tbg_ctx* c = new (std::nothrow) tbg_ctx();
   if (!c) return TBG_E_OOM;
   c->device = dev;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return TBG_E_DEVICE;
   }
-  uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 2;
+  // Every in-flight slot owns its two streams, so back-to-back submits
+  // overlap on the GPU (one batch's latency-bound stages fill the CUs the
+  // other leaves idle).
+  uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 3;
   c->slots.resize(nslots);
   for (auto& s : c->slots) {
+    if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&s.st2, hipStreamNonBlocking) != hipSuccess) {
+      tbg_destroy(c);
+      return TBG_E_DEVICE;
+    }
     for (auto& e : s.ev) hipEventCreate(&e);
     hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
   }
@@ -138,19 +146,23 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
 void tbg_destroy(tbg_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  if (c->stream) hipStreamSynchronize(c->stream);
   for (auto& s : c->slots) {
+    if (s.st) hipStreamSynchronize(s.st);
+    if (s.st2) hipStreamSynchronize(s.st2);
     if (s.h_in) hipHostFree(s.h_in);
     if (s.h_out) hipHostFree(s.h_out);
     if (s.d_in) hipFree(s.d_in);
     if (s.d_work) hipFree(s.d_work);
-    for (auto& e : s.ev) hipEventDestroy(e);
-    hipEventDestroy(s.done);
+    for (auto& e : s.ev)
+      if (e) hipEventDestroy(e);
+    if (s.done) hipEventDestroy(s.done);
+    if (s.st) hipStreamDestroy(s.st);
+    if (s.st2) hipStreamDestroy(s.st2);
   }
   if (c->d_pk) hipFree(c->d_pk);
   if (c->d_pk_status) hipFree(c->d_pk_status);
-  hipStreamDestroy(c->stream);
-  hipStreamDestroy(c->stream2);
+  if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -173,6 +185,10 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
       HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (auto& sl : c->slots) {  // in-flight batches may still read the old table
+      HIP_TRY(hipStreamSynchronize(sl.st));
+      HIP_TRY(hipStreamSynchronize(sl.st2));
+    }
     if (c->d_pk) hipFree(c->d_pk);
     if (c->d_pk_status) hipFree(c->d_pk_status);
     c->d_pk = npk;
@@ -204,8 +220,8 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
 // Events: ev[0] start, ev[1] decode done, ev[2] signature lines done,
 // ev[3]/ev[4] hash start/done and ev[5] H lines done (stream2), ev[6] verify
 // start, ev[7] verify done, ev[8] lagrange done, ev[9] aggregate done.
-static int launch_chain(tbg_ctx* c, const DevBatch& B, hipEvent_t* ev) {
-  hipStream_t st = c->stream, st2 = c->stream2;
+static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_t* ev) {
+  hipStream_t st = sl.st, st2 = sl.st2;
   const bool verify = B.op != TBG_OP_AGGREGATE;
   HIP_TRY(hipEventRecord(ev[0], st));
   HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
@@ -270,9 +286,11 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   if (rc != TBG_OK) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  // Least recently used free slot: a collected batch stays resident (for
+  // tbg_replay / tbg_fetch) until every other slot has been reused.
   Slot* s = nullptr;
   for (auto& x : c->slots)
-    if (!x.busy) { s = &x; break; }
+    if (!x.busy && (!s || x.ticket < s->ticket)) s = &x;
   if (!s) return TBG_E_BUSY;
 
   const bool verify = b->op != TBG_OP_AGGREGATE;
@@ -356,9 +374,11 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   B.duty_status = (int32_t*)(dw + w_dst);
   B.agg = dw + w_agg;
 
-  hipStream_t st = c->stream;
+  hipStream_t st = s->st;
+  // The resident pubkey table may have been (re)loaded on the utility stream.
+  HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpyAsync(s->d_in, s->h_in, in_bytes, hipMemcpyHostToDevice, st));
-  rc = launch_chain(c, B, s->ev);
+  rc = launch_chain(c, *s, B, s->ev);
   if (rc != TBG_OK) return rc;
   HIP_TRY(hipMemcpyAsync(s->h_out, dw + w_out, out_bytes, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipEventRecord(s->done, st));
@@ -412,19 +432,31 @@ int tbg_run(tbg_ctx* c, const tbg_batch* b, int32_t* pst, int32_t* dst, uint8_t*
   return tbg_collect(c, t, pst, dst, agg, 1);
 }
 
-int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms8) {
-  if (!c || iters == 0) return TBG_E_INVALID_ARG;
+int tbg_replay_multi(tbg_ctx* c, const tbg_ticket* tickets, uint32_t n_tickets, uint32_t iters, float* ms8) {
+  if (!c || !tickets || n_tickets == 0 || iters == 0) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  Slot* s = nullptr;
-  for (auto& x : c->slots)
-    if (!x.busy && x.ticket == t) { s = &x; break; }
-  if (!s) return TBG_E_TICKET;
+  std::vector<Slot*> sl(n_tickets, nullptr);
+  for (uint32_t j = 0; j < n_tickets; ++j) {
+    for (auto& x : c->slots)
+      if (!x.busy && x.ticket == tickets[j]) sl[j] = &x;
+    if (!sl[j]) return TBG_E_TICKET;
+    for (uint32_t k = 0; k < j; ++k)
+      if (sl[k] == sl[j]) return TBG_E_INVALID_ARG;
+  }
   HIP_TRY(hipSetDevice(c->device));
   std::vector<hipEvent_t> ev(10ull * iters);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   int rc = TBG_OK;
-  for (uint32_t k = 0; k < iters && rc == TBG_OK; ++k) rc = launch_chain(c, s->B, ev.data() + 10ull * k);
-  if (hipStreamSynchronize(c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  // Round-robin over the resident batches: launch k runs on the streams of
+  // slot k mod n_tickets, so up to n_tickets batches are in flight at once.
+  for (uint32_t k = 0; k < iters && rc == TBG_OK; ++k) {
+    Slot* s = sl[k % n_tickets];
+    rc = launch_chain(c, *s, s->B, ev.data() + 10ull * k);
+  }
+  for (uint32_t j = 0; j < n_tickets; ++j) {
+    if (hipStreamSynchronize(sl[j]->st) != hipSuccess) rc = TBG_E_DEVICE;
+    if (hipStreamSynchronize(sl[j]->st2) != hipSuccess) rc = TBG_E_DEVICE;
+  }
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (rc == TBG_OK) {
     for (uint32_t k = 0; k < iters; ++k) {
@@ -432,13 +464,20 @@ int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms8) {
       chain_times(ev.data() + 10ull * k, m);
       for (int j = 0; j < 7; ++j) acc[j] += m[j];
     }
-    hipEventElapsedTime(&acc[7], ev[0], ev[10ull * (iters - 1) + 9]);
+    // wall time: first launch's start to the latest chain end
+    for (uint32_t k = (iters > n_tickets ? iters - n_tickets : 0); k < iters; ++k) {
+      float w = 0;
+      hipEventElapsedTime(&w, ev[0], ev[10ull * k + 9]);
+      if (w > acc[7]) acc[7] = w;
+    }
     if (ms8) memcpy(ms8, acc, sizeof(acc));
     memcpy(c->last_ms, acc, sizeof(acc));
   }
   for (auto& e : ev) hipEventDestroy(e);
   return rc;
 }
+
+int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms8) { return tbg_replay_multi(c, &t, 1, iters, ms8); }
 
 int tbg_fetch(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg) {
   if (!c) return TBG_E_INVALID_ARG;
@@ -448,8 +487,8 @@ int tbg_fetch(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg
     if (!x.busy && x.ticket == t) { s = &x; break; }
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMemcpyAsync(s->h_out, s->d_work + s->w_out, s->out_bytes, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpyAsync(s->h_out, s->d_work + s->w_out, s->out_bytes, hipMemcpyDeviceToHost, s->st));
+  HIP_TRY(hipStreamSynchronize(s->st));
   const uint32_t np = s->n_partials, nd = s->n_duties;
   size_t o = 0;
   auto sec = [&](size_t bytes) { size_t at = o; o = align_up(o + bytes, 16); return at; };

@@ -63,7 +63,7 @@ class BatchResult:
 class Engine:
     """One context = one GPU (HIP device ordinal)."""
 
-    def __init__(self, device: int = 0, slots: int = 2):
+    def __init__(self, device: int = 0, slots: int = 3):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots)
         h = ctypes.c_void_p()
@@ -152,6 +152,13 @@ class Engine:
         """Re-run a collected batch's kernel chain on its resident inputs."""
         ms = np.zeros(8, dtype=np.float32)
         self._check(self._lib.tbg_replay(self._h, ticket, iters, _ptr(ms)), "tbg_replay")
+        return dict(zip(TIMING_KEYS, ms.tolist()))
+
+    def replay_multi(self, tickets, iters=1):
+        """Replay several resident batches round-robin, one in flight per slot."""
+        t = np.ascontiguousarray(np.asarray(tickets, dtype=np.uint64))
+        ms = np.zeros(8, dtype=np.float32)
+        self._check(self._lib.tbg_replay_multi(self._h, _ptr(t), len(t), iters, _ptr(ms)), "tbg_replay_multi")
         return dict(zip(TIMING_KEYS, ms.tolist()))
 
     def fetch(self, ticket, n_duties, n_partials) -> BatchResult:

@@ -75,7 +75,7 @@ typedef struct {
   uint32_t max_partials;  /* staging capacity hint (grows on demand)       */
   uint32_t max_duties;
   uint32_t max_msg_bytes;
-  uint32_t slots;         /* in-flight batches (0 -> 2)                    */
+  uint32_t slots;         /* in-flight batches, each on its own streams (0 -> 3) */
 } tbg_config;
 
 /* A batch of DV-duties in structure-of-arrays form.
@@ -124,6 +124,10 @@ int tbg_run(tbg_ctx* ctx, const tbg_batch* batch, int32_t* partial_status, int32
  * Blocks; ms8 receives per-kernel totals as in tbg_last_timings.  tbg_fetch
  * copies that slot's current outputs back (synchronous). */
 int tbg_replay(tbg_ctx* ctx, tbg_ticket ticket, uint32_t iters, float* ms8);
+/* Replay several collected batches round-robin, each on its own slot's
+ * streams, so up to n_tickets batches are in flight at once (the pipelined
+ * throughput of back-to-back submits).  ms8[7] is the wall time. */
+int tbg_replay_multi(tbg_ctx* ctx, const tbg_ticket* tickets, uint32_t n_tickets, uint32_t iters, float* ms8);
 int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
 
 /* Test-vector / benchmark-input generation on the GPU (not on the hot path):

@@ -25,7 +25,7 @@ def lib_path():
 def test_header_declares_the_boundary():
     names = declared()
     for must in ["tbg_init", "tbg_destroy", "tbg_load_pubkeys", "tbg_submit", "tbg_collect", "tbg_run",
-                 "tbg_replay", "tbg_fetch", "tbg_strerror", "tbg_sign", "tbg_sk_to_pk"]:
+                 "tbg_replay", "tbg_replay_multi", "tbg_fetch", "tbg_strerror", "tbg_sign", "tbg_sk_to_pk"]:
         assert must in names
 
 
