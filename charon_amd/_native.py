@@ -95,6 +95,9 @@ class TbgConfig(ctypes.Structure):
         ("max_duties", ctypes.c_uint32),
         ("max_msg_bytes", ctypes.c_uint32),
         ("slots", ctypes.c_uint32),
+        ("verify_mode", ctypes.c_uint32),
+        ("rlc_group", ctypes.c_uint32),
+        ("rlc_seed", ctypes.c_uint64),
     ]
 
 

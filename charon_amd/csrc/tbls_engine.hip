@@ -11,6 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <random>
 #include <vector>
 #include "tbls_launch.h"
 #include "bls_lines.h"
@@ -58,6 +59,9 @@ struct tbg_ctx {
   std::vector<Slot> slots;
   tbg_ticket next_ticket = 1;
   float last_ms[8] = {};
+  uint32_t rlc_group = 8;  // 0 = per-partial checks (TBG_VERIFY_EACH)
+  uint64_t rlc_seed = 0;   // 0 = OS randomness per batch
+  uint64_t seed_ctr = 0;
 };
 
 #define HIP_TRY(x)                       \
@@ -121,6 +125,11 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   tbg_ctx* c = new (std::nothrow) tbg_ctx();
   if (!c) return TBG_E_OOM;
   c->device = dev;
+  if (cfg && cfg->verify_mode == TBG_VERIFY_EACH) c->rlc_group = 0;
+  else if (cfg && cfg->verify_mode != TBG_VERIFY_RLC) { delete c; return TBG_E_INVALID_ARG; }
+  else if (cfg && cfg->rlc_group) c->rlc_group = cfg->rlc_group;
+  if (c->rlc_group > 4096) { delete c; return TBG_E_INVALID_ARG; }
+  c->rlc_seed = cfg ? cfg->rlc_seed : 0;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return TBG_E_DEVICE;
@@ -215,27 +224,30 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
 }
 
 // The kernel chain of one batch.  Per-message work (hash_to_G2, H(m) lines)
-// runs on stream2 concurrently with the per-signature work (decode, signature
-// lines) on stream; the quad verify joins both.
-// Events: ev[0] start, ev[1] decode done, ev[2] signature lines done,
-// ev[3]/ev[4] hash start/done and ev[5] H lines done (stream2), ev[6] verify
-// start, ev[7] verify done, ev[8] lagrange done, ev[9] aggregate done.
+// runs on st2 concurrently with the per-signature work (decode, RLC sums and
+// group lines) on st; the product checks join both.
+// Events: ev[0] start, ev[1] decode done, ev[2] combine done, ev[3]/ev[4]
+// hash start/done and ev[5] H lines done (st2), ev[6] verify start, ev[7]
+// verify done, ev[8] lagrange done, ev[9] aggregate done.
 static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_t* ev) {
   hipStream_t st = sl.st, st2 = sl.st2;
   const bool verify = B.op != TBG_OP_AGGREGATE;
+  const G1A* pk = (const G1A*)c->d_pk;
   HIP_TRY(hipEventRecord(ev[0], st));
   HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
   HIP_TRY(hipEventRecord(ev[3], st2));
-  launch_hash_msgs(B, st2);
+  if (verify) launch_hash_msgs(B, st2);
   HIP_TRY(hipEventRecord(ev[4], st2));
+  if (verify) launch_h_lines(B, st2);
+  HIP_TRY(hipEventRecord(ev[5], st2));
+  HIP_TRY(hipMemsetAsync(B.counters, 0, 4 * CNT_WORDS, st));
   launch_decode_sigs(B, st);
   HIP_TRY(hipEventRecord(ev[1], st));
-  if (verify) launch_lines(B, st, st2);
+  if (verify) launch_rlc_prepare(B, pk, (const int32_t*)c->d_pk_status, c->n_pk, st);
   HIP_TRY(hipEventRecord(ev[2], st));
-  HIP_TRY(hipEventRecord(ev[5], st2));
   HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
   HIP_TRY(hipEventRecord(ev[6], st));
-  if (verify) launch_verify(B, (const G1A*)c->d_pk, (const int32_t*)c->d_pk_status, c->n_pk, st);
+  if (verify) launch_rlc_check(B, pk, st);
   HIP_TRY(hipEventRecord(ev[7], st));
   if (B.op != TBG_OP_VERIFY) launch_lagrange(B, st);
   HIP_TRY(hipEventRecord(ev[8], st));
@@ -245,7 +257,7 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   return TBG_OK;
 }
 
-// [decode, hash, sig lines, H lines, verify, lagrange, aggregate, total]
+// [decode, hash, combine, H lines, verify, lagrange, aggregate, total]
 static void chain_times(hipEvent_t* e, float* ms) {
   hipEventElapsedTime(&ms[0], e[0], e[1]);
   hipEventElapsedTime(&ms[1], e[3], e[4]);
@@ -316,8 +328,19 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   size_t w_h_aff = sec(sizeof(G2A) * (size_t)nm);
   size_t w_h_st = sec(4ull * nm);
   size_t w_lam = sec(32ull * np);
-  size_t w_sl = sec(4ull * LINES_WORDS * np);
+  size_t w_sl = sec(verify ? 4ull * LINES_WORDS * np : 0);
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
+  const uint32_t G = verify ? c->rlc_group : 0;
+  const uint32_t ng = G ? (nd + G - 1) / G : 0;
+  size_t w_dvp = sec(G ? sizeof(G1A) * (size_t)nd : 0);
+  size_t w_dvs = sec(G ? sizeof(G2J) * (size_t)nd : 0);
+  size_t w_dvst = sec(G ? 4ull * nd : 0);
+  size_t w_gst = sec(4ull * ng);
+  size_t w_gl = sec(4ull * LINES_WORDS * ng);
+  size_t w_cnt = sec(4ull * CNT_WORDS);
+  size_t w_dvl = sec(G > 1 ? 4ull * nd : 0);
+  size_t w_dvlines = sec(G > 1 ? 4ull * LINES_WORDS * nd : 0);
+  size_t w_pl = sec(verify ? 4ull * np : 0);
   size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
   size_t w_pst = sec(4ull * np);
   size_t w_dst = sec(4ull * nd);
@@ -349,6 +372,7 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   }
 
   DevBatch B;
+  memset(&B, 0, sizeof(B));
   B.op = b->op;
   B.n_duties = nd;
   B.n_partials = np;
@@ -370,6 +394,36 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   B.lam = (uint32_t*)(dw + w_lam);
   B.sig_lines = (uint32_t*)(dw + w_sl);
   B.h_lines = (uint32_t*)(dw + w_hl);
+  B.rlc_group = G;
+  {
+    uint64_t k[4];
+    if (c->rlc_seed) {
+      uint64_t z = c->rlc_seed;  // splitmix64: fixed, reproducible scalars (tests only)
+      for (auto& w : k) {
+        z += 0x9E3779B97F4A7C15ull;
+        uint64_t x = z;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        w = x ^ (x >> 31);
+      }
+    } else {
+      std::random_device rd;  // the OS entropy source (getrandom / /dev/urandom)
+      for (auto& w : k) w = ((uint64_t)rd() << 32) ^ rd() ^ (++c->seed_ctr * 0x9E3779B97F4A7C15ull);
+    }
+    for (int j = 0; j < 4; ++j) {
+      B.rlc_seed[2 * j] = (uint32_t)(k[j] >> 32);
+      B.rlc_seed[2 * j + 1] = (uint32_t)k[j];
+    }
+  }
+  B.dv_p = (G1A*)(dw + w_dvp);
+  B.dv_s = (G2J*)(dw + w_dvs);
+  B.dv_state = (int32_t*)(dw + w_dvst);
+  B.grp_state = (int32_t*)(dw + w_gst);
+  B.grp_lines = (uint32_t*)(dw + w_gl);
+  B.counters = (uint32_t*)(dw + w_cnt);
+  B.dv_list = (uint32_t*)(dw + w_dvl);
+  B.dv_lines = (uint32_t*)(dw + w_dvlines);
+  B.part_list = (uint32_t*)(dw + w_pl);
   B.partial_status = (int32_t*)(dw + w_pst);
   B.duty_status = (int32_t*)(dw + w_dst);
   B.agg = dw + w_agg;

@@ -29,13 +29,29 @@ struct DevBatch {
   G2A* h_aff;
   int32_t* h_status;
   uint32_t* lam;       // [n_partials][8] scalar words
-  uint32_t* sig_lines;  // [n_partials][LINES_WORDS] Miller lines of each signature (-g1 folded in)
+  uint32_t* sig_lines;  // [n_partials][LINES_WORDS] Miller lines of listed signatures (-g1 folded in)
   uint32_t* h_lines;    // [n_msgs][LINES_WORDS] Miller lines of each H(m) (G1 factor left out)
+  // random-linear-combination verification (k_rlc.hip)
+  uint32_t rlc_seed[8];   // secret per-batch key of the scalars r_i
+  uint32_t rlc_group;     // duties per level-1 group; 0 = per-partial checks only
+  G1A* dv_p;              // [n_duties] sum r_i pk_i (affine)
+  G2J* dv_s;              // [n_duties] sum r_i sig_i
+  int32_t* dv_state;      // [n_duties] RLC_*
+  int32_t* grp_state;     // [n_groups] GRP_*
+  uint32_t* grp_lines;    // [n_groups][LINES_WORDS] lines of the group's S (-g1 folded in)
+  uint32_t* counters;     // [CNT_*] work-list lengths
+  uint32_t* dv_list;      // [n_duties] level-2 duties
+  uint32_t* dv_lines;     // [n_duties][LINES_WORDS] lines of S_d, by level-2 list position
+  uint32_t* part_list;    // [n_partials] level-3 partials (sig_lines by list position)
   // outputs
   int32_t* partial_status;
   int32_t* duty_status;
   uint8_t* agg;        // [n_duties][96]
 };
+
+enum RlcState : int32_t { RLC_NONE = 0, RLC_COMBINED = 1, RLC_EACH = 2 };
+enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3 };
+enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_WORDS = 4 };
 
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {
@@ -46,8 +62,9 @@ TBG_HD bool participates(uint32_t op, int32_t st) {
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, int32_t* status, hipStream_t st);
 void launch_decode_sigs(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);
-void launch_lines(const DevBatch& B, hipStream_t st_sig, hipStream_t st_h);
-void launch_verify(const DevBatch& B, const G1A* pk_aff, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+void launch_h_lines(const DevBatch& B, hipStream_t st);
+void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
 void launch_lagrange(const DevBatch& B, hipStream_t st);
 void launch_aggregate(const DevBatch& B, hipStream_t st);
 void launch_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* pk48, hipStream_t st);

@@ -7,6 +7,7 @@ numpy; every call goes to the HIP library (no CPU fallback).
 from __future__ import annotations
 
 import ctypes
+import itertools
 from dataclasses import dataclass
 
 import numpy as np
@@ -22,7 +23,8 @@ DS_INSUFFICIENT, DS_INSUFFICIENT_VALID = -20, -21
 DS_AGG_TOO_FEW, DS_AGG_DUPLICATE_ID, DS_AGG_IDENTITY, DS_DECODE = -22, -23, -24, -25
 OP_VERIFY, OP_AGGREGATE, OP_VERIFY_AGGREGATE = 1, 2, 3
 NO_PUBKEY = 0xFFFFFFFF
-TIMING_KEYS = ["decode", "hash", "sig_lines", "h_lines", "verify", "lagrange", "aggregate", "total"]
+TIMING_KEYS = ["decode", "hash", "combine", "h_lines", "verify", "lagrange", "aggregate", "total"]
+VERIFY_RLC, VERIFY_EACH = 0, 1
 E_PENDING = -6
 
 
@@ -60,17 +62,23 @@ class BatchResult:
     agg: np.ndarray             # uint8 [n_duties, 96]
 
 
+_serial = itertools.count(1)
+
+
 class Engine:
     """One context = one GPU (HIP device ordinal)."""
 
-    def __init__(self, device: int = 0, slots: int = 3):
+    def __init__(self, device: int = 0, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0,
+                 rlc_seed: int = 0):
         self._lib = _native.load()
-        cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots)
+        cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
+                                verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed)
         h = ctypes.c_void_p()
         rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
         self._check(rc, "tbg_init")
         self._h = h
         self.device = device
+        self.uid = next(_serial)  # never reused, unlike id(): keys per-context caches
         self._keep = {}
 
     def _check(self, rc, what):

@@ -105,7 +105,7 @@ class _PubkeyCache:
         self.ids = {}
 
     def ids_for(self, e: eng.Engine, keys):
-        cache = self.ids.setdefault(id(e), {})
+        cache = self.ids.setdefault(e.uid, {})
         missing = [k for k in dict.fromkeys(keys) if k not in cache]
         if missing:
             first, _ = e.load_pubkeys(b"".join(missing))

@@ -76,7 +76,17 @@ typedef struct {
   uint32_t max_duties;
   uint32_t max_msg_bytes;
   uint32_t slots;         /* in-flight batches, each on its own streams (0 -> 3) */
+  uint32_t verify_mode;   /* TBG_VERIFY_RLC (0, default) or TBG_VERIFY_EACH     */
+  uint32_t rlc_group;     /* duties per level-1 RLC group (0 -> 8)               */
+  uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests) */
 } tbg_config;
+
+/* Verification schedule.  Both give every partial the verdict of the exact
+ * per-item CoreVerify: RLC checks random linear combinations of groups of
+ * duties first and falls back to duties, then to single partials, on any
+ * failure (a false accept has probability <= 2^-64 per check). */
+#define TBG_VERIFY_RLC 0
+#define TBG_VERIFY_EACH 1
 
 /* A batch of DV-duties in structure-of-arrays form.
  * Duty d owns partials [duty_first[d], duty_first[d+1]) and message duty_msg[d];
@@ -139,8 +149,8 @@ int tbg_sign(tbg_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint8_t* msgs,
              uint32_t n_msgs, const uint32_t* item_msg, uint8_t* sig96);
 
 /* Last kernel timings of the context (milliseconds, HIP events on the
- * engine's streams): [decode, hash, sig lines, H lines, verify, lagrange,
- * aggregate, total]. */
+ * engine's streams): [decode, hash, combine (RLC sums + group lines),
+ * H lines, verify (all check levels), lagrange, aggregate, total]. */
 int tbg_last_timings(const tbg_ctx* ctx, float* ms8);
 
 #ifdef __cplusplus

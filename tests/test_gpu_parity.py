@@ -26,10 +26,22 @@ def load(name):
         return json.load(f)["vectors"]
 
 
-@pytest.fixture(scope="module")
-def engine():
+SCHEDULES = {
+    # exact per-partial CoreVerify for every candidate
+    "each": dict(verify_mode=1),
+    # random linear combinations: one duty per group (levels 1 -> 3)
+    "rlc1": dict(verify_mode=0, rlc_group=1, rlc_seed=0x5EED),
+    # the default: 8 duties per group, fresh OS randomness per batch
+    "rlc8": dict(verify_mode=0),
+    # large groups: most injected failures fall back through all three levels
+    "rlc64": dict(verify_mode=0, rlc_group=64, rlc_seed=0xC0FFEE),
+}
+
+
+@pytest.fixture(scope="module", params=list(SCHEDULES))
+def engine(request):
     from charon_amd import engine as eng
-    e = eng.Engine(0)
+    e = eng.Engine(0, **SCHEDULES[request.param])
     yield e
     e.close()
 
@@ -141,13 +153,13 @@ def _make_cluster_batch(engine, n_dv, t, n, seed, inject=0.0):
     return make_batch(engine, n_dv, t, n, seed, inject=inject)
 
 
-@pytest.mark.parametrize("n_dv,t,n", [(2000, 3, 4), (300, 7, 10)])
-def test_full_size_properties(engine, n_dv, t, n):
+@pytest.mark.parametrize("n_dv,t,n,inject", [(2000, 3, 4, 0.02), (300, 7, 10, 0.02), (512, 3, 4, 0.5)])
+def test_full_size_properties(engine, n_dv, t, n, inject):
     """At batch scale: every honest partial verifies, every aggregate equals
     the group signature sk * H(m) computed independently on the GPU, and an
     injected invalid partial is rejected without changing the aggregate."""
     from charon_amd import engine as eng
-    b = _make_cluster_batch(engine, n_dv, t, n, seed=11, inject=0.02)
+    b = _make_cluster_batch(engine, n_dv, t, n, seed=11, inject=inject)
     res = engine.run(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
                      duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
     expect_valid = ~b.injected
@@ -155,3 +167,33 @@ def test_full_size_properties(engine, n_dv, t, n):
     ok = res.duty_status == eng.DS_OK
     assert np.array_equal(ok, b.expect_ok)
     assert np.array_equal(res.agg[ok], b.group_sig[ok])
+
+
+def test_shared_messages_and_replay(engine):
+    """Committee-style batch: 64 duties share each message (the same H(m) is
+    paired with many combined keys inside one RLC group); replays of the
+    resident batch give the same verdicts and bytes."""
+    from charon_amd import engine as eng
+    b = _make_cluster_batch(engine, 256, 3, 4, seed=23, inject=0.01)
+    duty_msg = (np.arange(256) // 64).astype(np.uint32)
+    # re-sign so every duty signs its committee's message
+    msgs = [b.msgs[k * 64] for k in range(4)]
+    sk32 = b"".join(s.to_bytes(32, "big") for s in b.shares)
+    item_msg = np.repeat(duty_msg, 4)
+    sigs = engine.sign(sk32, msgs, item_msg)
+    wrong = engine.sign(sk32, [m[:-1] + bytes([m[-1] ^ 1]) for m in msgs], item_msg)
+    sigs = np.where(b.injected[:, None], wrong, sigs)
+    group = engine.sign(b"".join(s.to_bytes(32, "big") for s in b.secrets), msgs, duty_msg)
+    from charon_amd.engine import pack_messages
+    t = engine.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, sigs, b.identifiers, msgs=pack_messages(msgs),
+                      duty_msg=duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+    res = engine.collect(t)
+    assert np.array_equal(res.partial_status == eng.PS_VALID, ~b.injected)
+    ok = res.duty_status == eng.DS_OK
+    assert np.array_equal(ok, b.expect_ok)
+    assert np.array_equal(res.agg[ok], group[ok])
+    engine.replay(t, 2)
+    again = engine.fetch(t, 256, 1024)
+    assert np.array_equal(again.partial_status, res.partial_status)
+    assert np.array_equal(again.duty_status, res.duty_status)
+    assert np.array_equal(again.agg, res.agg)
