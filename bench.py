@@ -106,14 +106,18 @@ def main():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--inflight", type=int, default=3, help="resident batches replayed round-robin (engine slots)")
+    ap.add_argument("--inflight", type=int, default=4, help="resident batches replayed round-robin (engine slots)")
+    ap.add_argument("--verify-mode", type=int, default=0, help="0 = RLC groups with fallback, 1 = per-partial checks")
+    ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
+    ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()
     from charon_amd import engine as eng
     from tools.workload import make_batch
 
-    e = eng.Engine(local, slots=max(args.inflight, 1))
+    e = eng.Engine(local, slots=max(args.inflight, 1), verify_mode=args.verify_mode, rlc_group=args.rlc_group,
+                   rlc_chunk=args.rlc_chunk)
     # `inflight` independent 10k-DV batches stay resident, each in its own
     # engine slot (own HBM arena + own streams); step k replays batch
     # k mod inflight, so consecutive steps overlap on the GPU exactly as

@@ -98,6 +98,8 @@ class TbgConfig(ctypes.Structure):
         ("verify_mode", ctypes.c_uint32),
         ("rlc_group", ctypes.c_uint32),
         ("rlc_seed", ctypes.c_uint64),
+        ("rlc_chunk", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -119,6 +121,7 @@ SIGNATURES = {
     "tbg_replay_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_void_p]),
     "tbg_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "tbg_fetch_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "tbg_last_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_sk_to_pk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     "tbg_sign": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,

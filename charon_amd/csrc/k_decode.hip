@@ -5,18 +5,25 @@
 
 namespace tbg {
 
-__global__ void __launch_bounds__(64) k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, int32_t* status) {
+// Resident table entry: the key and [x]key (x the curve parameter), so the
+// RLC scalars of k_rlc.hip can be applied in base-x digits with the G1
+// endomorphism ([x^2] = -phi on G1) instead of 64-bit double-and-add.
+__global__ void __launch_bounds__(64) k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x,
+                                                       int32_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t b[48];
   for (int j = 0; j < 48; ++j) b[j] = pk48[48ull * i + j];
-  G1A a;
+  G1A a, ax;
   int32_t st = g1_decompress(b, a);
-  if (st != DEC_OK) {
+  if (st != DEC_OK || !jac_to_aff(jac_neg(jac_mul_xabs(jac_from_aff(a))), ax)) {
+    if (st == DEC_OK) st = DEC_IDENTITY;  // unreachable for a prime-order point
     a.x = fp_zero();
     a.y = fp_zero();
+    ax = a;
   }
   out[i] = a;
+  out_x[i] = ax;
   status[i] = st;
 }
 
@@ -36,8 +43,8 @@ __global__ void __launch_bounds__(64) k_decode_sigs(DevBatch B) {
   B.partial_status[i] = (st == DEC_OK) ? TBG_PS_NOT_VERIFIED : st;
 }
 
-void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, int32_t* status, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_decode_pubkeys, grid_for(n), dim3(kBlock), 0, st, pk48, n, out, status);
+void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_decode_pubkeys, grid_for(n), dim3(kBlock), 0, st, pk48, n, out, out_x, status);
 }
 void launch_decode_sigs(const DevBatch& B, hipStream_t st) {
   if (B.n_partials) hipLaunchKernelGGL(k_decode_sigs, grid_for(B.n_partials), dim3(kBlock), 0, st, B);

@@ -49,69 +49,105 @@ TBG_HD uint64_t rlc_scalar(const uint32_t (&seed)[8], uint32_t i) {
   return r ? r : 1;
 }
 
-// Candidate = decoded fine (status still NOT_VERIFIED) with a usable pubkey.
+// Candidate = decoded fine with a usable public key.  k_rlc_partial turns
+// non-candidates' NOT_VERIFIED into ERR_PUBKEY concurrently, so the test reads
+// the key table rather than trusting that transition to have happened.
+__device__ __forceinline__ bool rlc_usable(const DevBatch& B, uint32_t i, const int32_t* pk_status, uint32_t n_pk) {
+  int32_t st = B.partial_status[i];
+  if (st != TBG_PS_NOT_VERIFIED && st != TBG_PS_ERR_PUBKEY) return false;
+  uint32_t pid = B.pubkey_ids[i];
+  return pid < n_pk && pk_status[pid] == DEC_OK;
+}
 __device__ __forceinline__ bool rlc_candidate(const DevBatch& B, uint32_t i) {
   return B.partial_status[i] == TBG_PS_NOT_VERIFIED;
 }
 
+TBG_HD G2A g2_psi_aff(const G2A& a) {
+  return {fp2_mul(fp2_conj(a.x), fp2_from_const(PSI_X)), fp2_mul(fp2_conj(a.y), fp2_from_const(PSI_Y))};
+}
+
 // ------------------------------------------------------------------ level 0
-// One thread per duty: flag unusable pubkeys, then P_d and S_d by a
-// shared-doubling (Straus) 64-bit multi-scalar multiplication.
-__global__ void __launch_bounds__(64) k_rlc_combine(DevBatch B, const G1A* pk_aff, const int32_t* pk_status, uint32_t n_pk) {
+// One thread per partial: r_i s_i and r_i pk_i.  The 64 random bits are four
+// 16-bit digits a_k of r_i = a_0 + a_1 x + a_2 x^2 + a_3 x^3 (x the curve
+// parameter; distinct digit vectors give distinct r_i mod r because
+// 2^16 < |x| and 2^16 |x|^3 < r, so a false accept stays <= 2^-64).  The
+// subgroup check already proved psi(s) = [x] s for every decoded signature,
+// and on G1 [x^2] = -phi, so
+//   r_i s_i  = sum_k a_k psi^k(s_i)
+//   r_i pk_i = a_0 pk + a_1 [x]pk - a_2 phi(pk) - a_3 phi([x]pk)
+// are 16-bit four-point Straus products ([x]pk is resident in the key table).
+__global__ void __launch_bounds__(64) k_rlc_partial(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
+                                                    const int32_t* pk_status, uint32_t n_pk) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B.n_partials) return;
+  if (!rlc_candidate(B, i)) return;
+  uint32_t pid = B.pubkey_ids[i];
+  if (pid >= n_pk || pk_status[pid] != DEC_OK) {
+    B.partial_status[i] = TBG_PS_ERR_PUBKEY;
+    return;
+  }
+  uint32_t d = B.partial_duty[i];
+  bool lead = true;  // the duty's first candidate takes r = 1
+  for (uint32_t j = B.duty_first[d]; j < i && lead; ++j)
+    if (rlc_usable(B, j, pk_status, n_pk)) lead = false;
+  const G2A s0 = B.sig_aff[i];
+  const G1A p0 = pk_aff[pid];
+  if (lead) {
+    B.part_s[i] = jac_from_aff(s0);
+    B.part_p[i] = jac_from_aff(p0);
+    return;
+  }
+  uint64_t r = rlc_scalar(B.rlc_seed, i);
+  uint32_t a[4] = {(uint32_t)(r & 0xFFFF), (uint32_t)((r >> 16) & 0xFFFF), (uint32_t)((r >> 32) & 0xFFFF),
+                   (uint32_t)(r >> 48)};
+  G2A sq[4];
+  sq[0] = s0;
+  sq[1] = g2_psi_aff(sq[0]);
+  sq[2] = g2_psi_aff(sq[1]);
+  sq[3] = g2_psi_aff(sq[2]);
+  const G1A p1 = xpk_aff[pid];
+  const Fp beta = fp_from_const(G1_BETA);
+  G1A pq[4];
+  pq[0] = p0;
+  pq[1] = p1;
+  pq[2] = {fp_mul(p0.x, beta), fp_reduce(fp_neg(p0.y))};
+  pq[3] = {fp_mul(p1.x, beta), fp_reduce(fp_neg(p1.y))};
+  G2J S = jac_inf<Fp2>();
+  G1J P = jac_inf<Fp>();
+  bool started = false;
+  for (int bit = 15; bit >= 0; --bit) {
+    if (started) {
+      S = jac_dbl(S);
+      P = jac_dbl(P);
+    }
+    for (int k = 0; k < 4; ++k) {
+      if ((a[k] >> bit) & 1) {
+        S = jac_add_aff(S, sq[k]);
+        P = jac_add_aff(P, pq[k]);
+        started = true;
+      }
+    }
+  }
+  B.part_s[i] = S;
+  B.part_p[i] = P;
+}
+
+// One thread per duty: P_d = sum r_i pk_i (affine) and S_d = sum r_i s_i.
+__global__ void __launch_bounds__(64) k_rlc_duty_sum(DevBatch B) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= B.n_duties) return;
-  uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
+  G1J P = jac_inf<Fp>();
+  G2J S = jac_inf<Fp2>();
   int cand = 0;
-  for (uint32_t i = first; i < last; ++i) {
+  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) {
     if (!rlc_candidate(B, i)) continue;
-    uint32_t pid = B.pubkey_ids[i];
-    if (pid >= n_pk || pk_status[pid] != DEC_OK) {
-      B.partial_status[i] = TBG_PS_ERR_PUBKEY;
-      continue;
-    }
+    P = jac_add(P, B.part_p[i]);
+    S = jac_add(S, B.part_s[i]);
     ++cand;
   }
   if (cand == 0) {
     B.dv_state[d] = RLC_NONE;
     return;
-  }
-  // Chunks of up to 8 candidates: the scalars of a chunk stay in registers
-  // and its 64 doublings are shared (Straus); chunk sums are added up.
-  G1J P = jac_inf<Fp>();
-  G2J S = jac_inf<Fp2>();
-  bool lead = true;
-  uint32_t i = first;
-  while (i < last) {
-    uint32_t idx[8];
-    uint64_t r[8];
-    int k = 0;
-    for (; i < last && k < 8; ++i) {
-      if (!rlc_candidate(B, i)) continue;
-      idx[k] = i;
-      r[k] = lead ? 1ull : rlc_scalar(B.rlc_seed, i);
-      lead = false;
-      ++k;
-    }
-    uint64_t any = 0;
-    for (int j = 0; j < k; ++j) any |= r[j];
-    G1J Pc = jac_inf<Fp>();
-    G2J Sc = jac_inf<Fp2>();
-    bool started = false;
-    for (int bit = 63 - __builtin_clzll(any | 1); bit >= 0; --bit) {
-      if (started) {
-        Pc = jac_dbl(Pc);
-        Sc = jac_dbl(Sc);
-      }
-      for (int j = 0; j < k; ++j) {
-        if ((r[j] >> bit) & 1) {
-          Pc = jac_add_aff(Pc, pk_aff[B.pubkey_ids[idx[j]]]);
-          Sc = jac_add_aff(Sc, B.sig_aff[idx[j]]);
-          started = true;
-        }
-      }
-    }
-    P = jac_add(P, Pc);
-    S = jac_add(S, Sc);
   }
   G1A Pa;
   if (!jac_to_aff(P, Pa) || jac_is_inf(S)) {
@@ -161,23 +197,38 @@ __device__ __forceinline__ Fp4 quad_line_folded(const Fp4& f, const uint32_t* li
   return quad_line(f, a.l0, a.l1, a.l4);
 }
 
-// Level 1: one quad per group.
-__global__ void __launch_bounds__(64) k_rlc_check_groups(DevBatch B) {
+// Quad-layout Fp12 in HBM: lane q < 3 owns one Fp4 (4 NL words).
+constexpr int QUAD_WORDS = 4 * NL;
+__device__ __forceinline__ void quad_store(uint32_t* dst, const Fp4& A) {
+  int q = quad_lane();
+  if ((threadIdx.x & 3) == 3) return;
+  const Fp* f[4] = {&A.a.c0, &A.a.c1, &A.b.c0, &A.b.c1};
+  for (int k = 0; k < 4; ++k)
+    for (int j = 0; j < NL; ++j) dst[QUAD_WORDS * q + k * NL + j] = f[k]->l[j];
+}
+__device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
+  int q = quad_lane();
+  Fp4 A;
+  Fp* f[4] = {&A.a.c0, &A.a.c1, &A.b.c0, &A.b.c1};
+  for (int k = 0; k < 4; ++k)
+    for (int j = 0; j < NL; ++j) f[k]->l[j] = src[QUAD_WORDS * q + k * NL + j];
+  return A;
+}
+
+// Level 1, Miller part: one quad per (group, chunk of rlc_chunk duties); the
+// group's S pair rides in chunk 0.  Chunks share nothing but the final
+// exponentiation, so a group's pairs are spread over several quads.
+__global__ void __launch_bounds__(64) k_rlc_miller_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t g = t >> 2;
-  uint32_t G = B.rlc_group;
+  uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
-  if (g >= n_groups) return;
-  const bool lead = (t & 3) == 0;
-  int32_t gs = B.grp_state[g];
-  if (gs != GRP_LINES) return;  // empty groups have nothing to resolve; GRP_FAIL stays failed
-  uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
-  for (uint32_t d = d0; d < d1; ++d) {
-    if (B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] != 0) {
-      if (lead) B.grp_state[g] = GRP_FAIL;  // resolved per duty
-      return;
-    }
-  }
+  uint32_t nch = (G + C - 1) / C;
+  uint32_t qd = t >> 2;
+  if (qd >= n_groups * nch) return;
+  uint32_t g = qd / nch, c = qd % nch;
+  if (B.grp_state[g] != GRP_LINES) return;
+  uint32_t gd1 = min(g * G + G, B.n_duties);
+  uint32_t d0 = g * G + c * C, d1 = min(d0 + C, gd1);
   const uint32_t* ls = B.grp_lines + (size_t)LINES_WORDS * g;
   Fp4 f = quad_one();
   int idx = 0;
@@ -185,14 +236,40 @@ __global__ void __launch_bounds__(64) k_rlc_check_groups(DevBatch B) {
     if (b != 62) f = quad_sqr(f);
     int steps = ((X_ABS >> b) & 1) ? 2 : 1;
     for (int s = 0; s < steps; ++s, ++idx) {
-      f = quad_line_folded(f, ls, idx);
+      if (c == 0) f = quad_line_folded(f, ls, idx);
       for (uint32_t d = d0; d < d1; ++d) {
         if (B.dv_state[d] != RLC_COMBINED) continue;
+        uint32_t m = B.duty_msg[d];
+        if (B.h_status[m] != 0) continue;  // the group fails in k_rlc_group_final
         const G1A& P = B.dv_p[d];
-        f = quad_line_at(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, fp_reduce(fp_neg(P.x)), P.y);
+        f = quad_line_at(f, B.h_lines + (size_t)LINES_WORDS * m, idx, fp_reduce(fp_neg(P.x)), P.y);
       }
     }
   }
+  quad_store(B.chunk_f + (size_t)3 * QUAD_WORDS * qd, f);
+}
+
+// Level 1, final part: one quad per group multiplies its chunks' products
+// and runs the one final exponentiation of the group.
+__global__ void __launch_bounds__(64) k_rlc_group_final(DevBatch B) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t G = B.rlc_group, C = B.rlc_chunk;
+  uint32_t n_groups = (B.n_duties + G - 1) / G;
+  uint32_t nch = (G + C - 1) / C;
+  uint32_t g = t >> 2;
+  if (g >= n_groups) return;
+  const bool lead = (t & 3) == 0;
+  if (B.grp_state[g] != GRP_LINES) return;  // empty groups have nothing to resolve; GRP_FAIL stays failed
+  uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
+  for (uint32_t d = d0; d < d1; ++d) {
+    if (B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] != 0) {
+      if (lead) B.grp_state[g] = GRP_FAIL;  // resolved per duty
+      return;
+    }
+  }
+  const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nch * g;
+  Fp4 f = quad_load(base);
+  for (uint32_t c = 1; c < nch; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
   f = quad_final_exp(quad_conj(f));
   bool ok = quad_is_one(f);
   if (lead) B.grp_state[g] = ok ? GRP_OK : GRP_FAIL;
@@ -227,7 +304,7 @@ __global__ void __launch_bounds__(64) k_rlc_duty_lines(DevBatch B) {
   if (k >= B.counters[CNT_DUTIES]) return;
   uint32_t d = B.dv_list[k];
   G2A Sa;
-  if (!jac_to_aff(B.dv_s[d], Sa)) return;  // excluded in k_rlc_combine
+  if (!jac_to_aff(B.dv_s[d], Sa)) return;  // excluded in k_rlc_duty_sum
   Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
   g2_lines(Sa, nx, fp_from_const(G1_NEG_Y), B.dv_lines + (size_t)LINES_WORDS * k);
 }
@@ -313,13 +390,16 @@ __global__ void __launch_bounds__(64) k_verify_list(DevBatch B, const G1A* pk_af
   if (lead) B.partial_status[i] = ok ? TBG_PS_VALID : TBG_PS_INVALID;
 }
 
-void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
+void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
+                        hipStream_t st) {
   if (!B.n_duties) return;
   if (B.rlc_group == 0) {
     if (B.n_partials) hipLaunchKernelGGL(k_list_all_partials, grid_for(B.n_partials), dim3(kBlock), 0, st, B, pk_status, n_pk);
     return;
   }
-  hipLaunchKernelGGL(k_rlc_combine, grid_for(B.n_duties), dim3(kBlock), 0, st, B, pk_aff, pk_status, n_pk);
+  if (B.n_partials)
+    hipLaunchKernelGGL(k_rlc_partial, grid_for(B.n_partials), dim3(kBlock), 0, st, B, pk_aff, xpk_aff, pk_status, n_pk);
+  hipLaunchKernelGGL(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), 0, st, B);
   uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
   hipLaunchKernelGGL(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), 0, st, B);
 }
@@ -328,7 +408,9 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
   if (!B.n_duties) return;
   if (B.rlc_group != 0) {
     uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
-    hipLaunchKernelGGL(k_rlc_check_groups, grid_for(4 * n_groups), dim3(kBlock), 0, st, B);
+    uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
+    hipLaunchKernelGGL(k_rlc_miller_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), 0, st, B);
+    hipLaunchKernelGGL(k_rlc_group_final, grid_for(4 * n_groups), dim3(kBlock), 0, st, B);
     hipLaunchKernelGGL(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), 0, st, B);
     if (B.rlc_group > 1) {
       hipLaunchKernelGGL(k_rlc_duty_lines, grid_for(B.n_duties), dim3(kBlock), 0, st, B);

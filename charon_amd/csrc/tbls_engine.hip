@@ -54,12 +54,14 @@ struct tbg_ctx {
   hipStream_t stream = nullptr;  // utility stream (pubkey table, test-vector generation)
   std::mutex mu;
   G1A* d_pk = nullptr;
+  G1A* d_xpk = nullptr;  // [x] pk per entry (k_decode_pubkeys)
   int32_t* d_pk_status = nullptr;
   uint32_t n_pk = 0, cap_pk = 0;
   std::vector<Slot> slots;
   tbg_ticket next_ticket = 1;
   float last_ms[8] = {};
   uint32_t rlc_group = 8;  // 0 = per-partial checks (TBG_VERIFY_EACH)
+  uint32_t rlc_chunk = 2;
   uint64_t rlc_seed = 0;   // 0 = OS randomness per batch
   uint64_t seed_ctr = 0;
 };
@@ -128,7 +130,8 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   if (cfg && cfg->verify_mode == TBG_VERIFY_EACH) c->rlc_group = 0;
   else if (cfg && cfg->verify_mode != TBG_VERIFY_RLC) { delete c; return TBG_E_INVALID_ARG; }
   else if (cfg && cfg->rlc_group) c->rlc_group = cfg->rlc_group;
-  if (c->rlc_group > 4096) { delete c; return TBG_E_INVALID_ARG; }
+  if (cfg && cfg->rlc_chunk) c->rlc_chunk = cfg->rlc_chunk;
+  if (c->rlc_group > 4096 || c->rlc_chunk > 4096) { delete c; return TBG_E_INVALID_ARG; }
   c->rlc_seed = cfg ? cfg->rlc_seed : 0;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -170,6 +173,7 @@ void tbg_destroy(tbg_ctx* c) {
     if (s.st2) hipStreamDestroy(s.st2);
   }
   if (c->d_pk) hipFree(c->d_pk);
+  if (c->d_xpk) hipFree(c->d_xpk);
   if (c->d_pk_status) hipFree(c->d_pk_status);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -186,11 +190,14 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   if (need > c->cap_pk) {
     uint32_t ncap = need + need / 2 + 1024;
     G1A* npk = nullptr;
+    G1A* nxpk = nullptr;
     int32_t* nst = nullptr;
     if (hipMalloc(&npk, sizeof(G1A) * (size_t)ncap) != hipSuccess) return TBG_E_OOM;
-    if (hipMalloc(&nst, sizeof(int32_t) * (size_t)ncap) != hipSuccess) { hipFree(npk); return TBG_E_OOM; }
+    if (hipMalloc(&nxpk, sizeof(G1A) * (size_t)ncap) != hipSuccess) { hipFree(npk); return TBG_E_OOM; }
+    if (hipMalloc(&nst, sizeof(int32_t) * (size_t)ncap) != hipSuccess) { hipFree(npk); hipFree(nxpk); return TBG_E_OOM; }
     if (c->n_pk) {
       HIP_TRY(hipMemcpyAsync(npk, c->d_pk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(nxpk, c->d_xpk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
       HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -199,8 +206,10 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
       HIP_TRY(hipStreamSynchronize(sl.st2));
     }
     if (c->d_pk) hipFree(c->d_pk);
+    if (c->d_xpk) hipFree(c->d_xpk);
     if (c->d_pk_status) hipFree(c->d_pk_status);
     c->d_pk = npk;
+    c->d_xpk = nxpk;
     c->d_pk_status = nst;
     c->cap_pk = ncap;
   }
@@ -211,7 +220,7 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   int rc = TBG_OK;
   if (hipMemcpyAsync(d_bytes, pk48, 48ull * count, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
   if (rc == TBG_OK) {
-    launch_decode_pubkeys(d_bytes, count, c->d_pk + c->n_pk, c->d_pk_status + c->n_pk, c->stream);
+    launch_decode_pubkeys(d_bytes, count, c->d_pk + c->n_pk, c->d_xpk + c->n_pk, c->d_pk_status + c->n_pk, c->stream);
     if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
   }
   if (rc == TBG_OK && status &&
@@ -243,7 +252,7 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   HIP_TRY(hipMemsetAsync(B.counters, 0, 4 * CNT_WORDS, st));
   launch_decode_sigs(B, st);
   HIP_TRY(hipEventRecord(ev[1], st));
-  if (verify) launch_rlc_prepare(B, pk, (const int32_t*)c->d_pk_status, c->n_pk, st);
+  if (verify) launch_rlc_prepare(B, pk, (const G1A*)c->d_xpk, (const int32_t*)c->d_pk_status, c->n_pk, st);
   HIP_TRY(hipEventRecord(ev[2], st));
   HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
   HIP_TRY(hipEventRecord(ev[6], st));
@@ -332,6 +341,11 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
   const uint32_t G = verify ? c->rlc_group : 0;
   const uint32_t ng = G ? (nd + G - 1) / G : 0;
+  const uint32_t C = c->rlc_chunk < G ? c->rlc_chunk : (G ? G : 1);
+  const uint32_t nch = G ? (G + C - 1) / C : 0;
+  size_t w_pp = sec(G ? sizeof(G1J) * (size_t)np : 0);
+  size_t w_ps = sec(G ? sizeof(G2J) * (size_t)np : 0);
+  size_t w_cf = sec(G ? 4ull * 3 * 4 * NL * ng * nch : 0);
   size_t w_dvp = sec(G ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_dvs = sec(G ? sizeof(G2J) * (size_t)nd : 0);
   size_t w_dvst = sec(G ? 4ull * nd : 0);
@@ -415,6 +429,10 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
       B.rlc_seed[2 * j + 1] = (uint32_t)k[j];
     }
   }
+  B.rlc_chunk = C;
+  B.part_p = (G1J*)(dw + w_pp);
+  B.part_s = (G2J*)(dw + w_ps);
+  B.chunk_f = (uint32_t*)(dw + w_cf);
   B.dv_p = (G1A*)(dw + w_dvp);
   B.dv_s = (G2J*)(dw + w_dvs);
   B.dv_state = (int32_t*)(dw + w_dvst);
@@ -550,6 +568,27 @@ int tbg_fetch(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg
   if (pst) memcpy(pst, s->h_out + o_pst, 4ull * np);
   if (dst) memcpy(dst, s->h_out + o_dst, 4ull * nd);
   if (agg) memcpy(agg, s->h_out + o_agg, 96ull * nd);
+  return TBG_OK;
+}
+
+int tbg_fetch_stats(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
+  if (!c || !out4) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = nullptr;
+  for (auto& x : c->slots)
+    if (!x.busy && x.ticket == t) { s = &x; break; }
+  if (!s) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  uint32_t cnt[CNT_WORDS] = {0, 0, 0, 0};
+  if (s->op != TBG_OP_AGGREGATE) {
+    HIP_TRY(hipMemcpyAsync(cnt, s->B.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
+    HIP_TRY(hipStreamSynchronize(s->st));
+  }
+  uint32_t ng = s->B.rlc_group ? (s->n_duties + s->B.rlc_group - 1) / s->B.rlc_group : 0;
+  out4[0] = ng;
+  out4[1] = cnt[CNT_DUTIES];
+  out4[2] = cnt[CNT_PARTIALS];
+  out4[3] = s->B.rlc_group;
   return TBG_OK;
 }
 

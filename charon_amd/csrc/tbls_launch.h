@@ -34,6 +34,10 @@ struct DevBatch {
   // random-linear-combination verification (k_rlc.hip)
   uint32_t rlc_seed[8];   // secret per-batch key of the scalars r_i
   uint32_t rlc_group;     // duties per level-1 group; 0 = per-partial checks only
+  G1J* part_p;            // [n_partials] r_i pk_i
+  G2J* part_s;            // [n_partials] r_i sig_i
+  uint32_t rlc_chunk;     // duties per level-1 Miller chunk (quads per group = ceil(G / chunk))
+  uint32_t* chunk_f;      // [n_groups * chunks][3][4 NL] Miller products of the chunks (quad layout)
   G1A* dv_p;              // [n_duties] sum r_i pk_i (affine)
   G2J* dv_s;              // [n_duties] sum r_i sig_i
   int32_t* dv_state;      // [n_duties] RLC_*
@@ -59,11 +63,12 @@ TBG_HD bool participates(uint32_t op, int32_t st) {
 }
 
 // launchers (asynchronous on `st`)
-void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, int32_t* status, hipStream_t st);
+void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st);
 void launch_decode_sigs(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);
 void launch_h_lines(const DevBatch& B, hipStream_t st);
-void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
+                        hipStream_t st);
 void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
 void launch_lagrange(const DevBatch& B, hipStream_t st);
 void launch_aggregate(const DevBatch& B, hipStream_t st);

@@ -69,10 +69,11 @@ class Engine:
     """One context = one GPU (HIP device ordinal)."""
 
     def __init__(self, device: int = 0, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0,
-                 rlc_seed: int = 0):
+                 rlc_seed: int = 0, rlc_chunk: int = 0):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
-                                verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed)
+                                verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
+                                rlc_chunk=rlc_chunk)
         h = ctypes.c_void_p()
         rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
         self._check(rc, "tbg_init")
@@ -175,6 +176,12 @@ class Engine:
         agg = np.zeros((n_duties, 96), dtype=np.uint8)
         self._check(self._lib.tbg_fetch(self._h, ticket, _ptr(ps), _ptr(ds), _ptr(agg)), "tbg_fetch")
         return BatchResult(ps, ds, agg)
+
+    def stats(self, ticket) -> dict:
+        """Verification work of the batch's last run (how much fell back)."""
+        out = np.zeros(4, dtype=np.uint32)
+        self._check(self._lib.tbg_fetch_stats(self._h, ticket, _ptr(out)), "tbg_fetch_stats")
+        return dict(zip(["groups", "duty_checks", "partial_checks", "group_size"], out.tolist()))
 
     def timings(self):
         ms = np.zeros(8, dtype=np.float32)

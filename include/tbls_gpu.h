@@ -79,6 +79,8 @@ typedef struct {
   uint32_t verify_mode;   /* TBG_VERIFY_RLC (0, default) or TBG_VERIFY_EACH     */
   uint32_t rlc_group;     /* duties per level-1 RLC group (0 -> 8)               */
   uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests) */
+  uint32_t rlc_chunk;     /* duties per Miller-loop quad inside a group (0 -> 2)  */
+  uint32_t reserved;
 } tbg_config;
 
 /* Verification schedule.  Both give every partial the verdict of the exact
@@ -139,6 +141,10 @@ int tbg_replay(tbg_ctx* ctx, tbg_ticket ticket, uint32_t iters, float* ms8);
  * throughput of back-to-back submits).  ms8[7] is the wall time. */
 int tbg_replay_multi(tbg_ctx* ctx, const tbg_ticket* tickets, uint32_t n_tickets, uint32_t iters, float* ms8);
 int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
+/* Verification work of a collected batch's last run: out4 = [level-1 groups,
+ * duties re-checked alone (level 2), partials checked one by one (level 3),
+ * duties per group (0 = TBG_VERIFY_EACH)]. */
+int tbg_fetch_stats(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out4);
 
 /* Test-vector / benchmark-input generation on the GPU (not on the hot path):
  * tbls.Sign / PartialSign (reference tbls/tss.go:200-217) and

@@ -35,6 +35,8 @@ SCHEDULES = {
     "rlc8": dict(verify_mode=0),
     # large groups: most injected failures fall back through all three levels
     "rlc64": dict(verify_mode=0, rlc_group=64, rlc_seed=0xC0FFEE),
+    # odd group / chunk sizes: ragged last group, chunks of 3 duties
+    "rlc7c3": dict(verify_mode=0, rlc_group=7, rlc_chunk=3, rlc_seed=77),
 }
 
 
@@ -167,6 +169,22 @@ def test_full_size_properties(engine, n_dv, t, n, inject):
     ok = res.duty_status == eng.DS_OK
     assert np.array_equal(ok, b.expect_ok)
     assert np.array_equal(res.agg[ok], b.group_sig[ok])
+
+
+def test_clean_batch_needs_no_fallback(engine):
+    """Honest partials pass at level 1: the RLC combination itself is right
+    (a wrong scalar identity would still give right verdicts, via fallback)."""
+    from charon_amd import engine as eng
+    b = _make_cluster_batch(engine, 1000, 3, 4, seed=5)
+    t = engine.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
+                      duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+    res = engine.collect(t)
+    assert (res.partial_status == eng.PS_VALID).all()
+    st = engine.stats(t)
+    if st["group_size"]:
+        assert st["duty_checks"] == 0 and st["partial_checks"] == 0, st
+    else:
+        assert st["partial_checks"] == 4000
 
 
 def test_shared_messages_and_replay(engine):
