@@ -25,6 +25,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# The engine keeps several batches in flight, one HIP stream each; the HIP
+# runtime multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
+# default), and streams sharing a queue serialise.  It is read once, at HIP
+# initialisation, so it is set before anything touches the GPU (the Go host
+# process sets it in its environment).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 METRIC = "verified+aggregated 3-of-4 threshold BLS sigs/sec at 1/2/4/8 MI355X"
 # Measured on MI355X by tools/microbench/valu_rates.hip (2 waves/SIMD, 8
 # independent chains): v_mad_u64_u32 = 32.1 T lane-ops/s.  See DESIGN.md.
@@ -98,7 +105,7 @@ def cpu_baseline(batch, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--dvs", type=int, default=10000)
     ap.add_argument("--t", type=int, default=3)
@@ -106,10 +113,11 @@ def main():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--inflight", type=int, default=4, help="resident batches replayed round-robin (engine slots)")
+    ap.add_argument("--inflight", type=int, default=8, help="resident batches replayed round-robin (engine slots)")
     ap.add_argument("--verify-mode", type=int, default=0, help="0 = RLC groups with fallback, 1 = per-partial checks")
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
+    ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()
@@ -117,7 +125,7 @@ def main():
     from tools.workload import make_batch
 
     e = eng.Engine(local, slots=max(args.inflight, 1), verify_mode=args.verify_mode, rlc_group=args.rlc_group,
-                   rlc_chunk=args.rlc_chunk)
+                   rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot)
     # `inflight` independent 10k-DV batches stay resident, each in its own
     # engine slot (own HBM arena + own streams); step k replays batch
     # k mod inflight, so consecutive steps overlap on the GPU exactly as
@@ -177,7 +185,7 @@ def main():
         "data": "synthetic (seeded shares/pubshares/signatures generated on the GPU)",
         "config": {"workload": f"config2: {args.t}-of-{args.n}, {args.dvs} DVs x 1 attestation per GPU",
                    "partials_per_step_per_gpu": args.dvs * args.n, "parallelism": f"shard{ws}",
-                   "inflight_batches": args.inflight},
+                   "inflight_batches": args.inflight, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),
         "roofline": roofline,

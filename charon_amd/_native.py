@@ -99,7 +99,7 @@ class TbgConfig(ctypes.Structure):
         ("rlc_group", ctypes.c_uint32),
         ("rlc_seed", ctypes.c_uint64),
         ("rlc_chunk", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("streams_per_slot", ctypes.c_uint32),
     ]
 
 

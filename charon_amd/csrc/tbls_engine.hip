@@ -20,6 +20,8 @@ using namespace tbg;
 
 namespace {
 
+constexpr int kChainEvents = 11;
+
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct Slot {
@@ -40,7 +42,7 @@ struct Slot {
   size_t out_bytes = 0;
   hipStream_t st = nullptr;   // per-signature chain (decode, lines, verify, aggregate)
   hipStream_t st2 = nullptr;  // per-message chain (hash_to_G2, H(m) lines), joins st before verify
-  hipEvent_t ev[10] = {};  // see launch_chain
+  hipEvent_t ev[kChainEvents] = {};  // see launch_chain
   hipEvent_t done = nullptr;
   float ms[8] = {};
   tbg::DevBatch B{};           // device view of the last batch (resident until the slot is reused)
@@ -142,12 +144,19 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // other leaves idle).
   uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 3;
   c->slots.resize(nslots);
+  // One stream per slot by default: the HIP runtime maps streams onto a
+  // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), so concurrency
+  // comes from several batches in flight, one queue each.  Two streams
+  // per slot also overlap a batch's hash_to_G2 with its decode (lower
+  // single-batch latency when queues are plentiful).
+  const bool two = cfg && cfg->streams_per_slot >= 2;
   for (auto& s : c->slots) {
     if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&s.st2, hipStreamNonBlocking) != hipSuccess) {
+        (two && hipStreamCreateWithFlags(&s.st2, hipStreamNonBlocking) != hipSuccess)) {
       tbg_destroy(c);
       return TBG_E_DEVICE;
     }
+    if (!two) s.st2 = s.st;
     for (auto& e : s.ev) hipEventCreate(&e);
     hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
   }
@@ -161,7 +170,7 @@ void tbg_destroy(tbg_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   for (auto& s : c->slots) {
     if (s.st) hipStreamSynchronize(s.st);
-    if (s.st2) hipStreamSynchronize(s.st2);
+    if (s.st2 && s.st2 != s.st) hipStreamSynchronize(s.st2);
     if (s.h_in) hipHostFree(s.h_in);
     if (s.h_out) hipHostFree(s.h_out);
     if (s.d_in) hipFree(s.d_in);
@@ -169,8 +178,8 @@ void tbg_destroy(tbg_ctx* c) {
     for (auto& e : s.ev)
       if (e) hipEventDestroy(e);
     if (s.done) hipEventDestroy(s.done);
+    if (s.st2 && s.st2 != s.st) hipStreamDestroy(s.st2);
     if (s.st) hipStreamDestroy(s.st);
-    if (s.st2) hipStreamDestroy(s.st2);
   }
   if (c->d_pk) hipFree(c->d_pk);
   if (c->d_xpk) hipFree(c->d_xpk);
@@ -237,7 +246,7 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
 // group lines) on st; the product checks join both.
 // Events: ev[0] start, ev[1] decode done, ev[2] combine done, ev[3]/ev[4]
 // hash start/done and ev[5] H lines done (st2), ev[6] verify start, ev[7]
-// verify done, ev[8] lagrange done, ev[9] aggregate done.
+// verify done, ev[8] lagrange done, ev[9] aggregate done, ev[10] decode start.
 static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_t* ev) {
   hipStream_t st = sl.st, st2 = sl.st2;
   const bool verify = B.op != TBG_OP_AGGREGATE;
@@ -249,6 +258,7 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   HIP_TRY(hipEventRecord(ev[4], st2));
   if (verify) launch_h_lines(B, st2);
   HIP_TRY(hipEventRecord(ev[5], st2));
+  HIP_TRY(hipEventRecord(ev[10], st));
   HIP_TRY(hipMemsetAsync(B.counters, 0, 4 * CNT_WORDS, st));
   launch_decode_sigs(B, st);
   HIP_TRY(hipEventRecord(ev[1], st));
@@ -268,7 +278,7 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
 
 // [decode, hash, combine, H lines, verify, lagrange, aggregate, total]
 static void chain_times(hipEvent_t* e, float* ms) {
-  hipEventElapsedTime(&ms[0], e[0], e[1]);
+  hipEventElapsedTime(&ms[0], e[10], e[1]);
   hipEventElapsedTime(&ms[1], e[3], e[4]);
   hipEventElapsedTime(&ms[2], e[1], e[2]);
   hipEventElapsedTime(&ms[3], e[4], e[5]);
@@ -516,14 +526,14 @@ int tbg_replay_multi(tbg_ctx* c, const tbg_ticket* tickets, uint32_t n_tickets, 
       if (sl[k] == sl[j]) return TBG_E_INVALID_ARG;
   }
   HIP_TRY(hipSetDevice(c->device));
-  std::vector<hipEvent_t> ev(10ull * iters);
+  std::vector<hipEvent_t> ev((size_t)kChainEvents * iters);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   int rc = TBG_OK;
   // Round-robin over the resident batches: launch k runs on the streams of
   // slot k mod n_tickets, so up to n_tickets batches are in flight at once.
   for (uint32_t k = 0; k < iters && rc == TBG_OK; ++k) {
     Slot* s = sl[k % n_tickets];
-    rc = launch_chain(c, *s, s->B, ev.data() + 10ull * k);
+    rc = launch_chain(c, *s, s->B, ev.data() + (size_t)kChainEvents * k);
   }
   for (uint32_t j = 0; j < n_tickets; ++j) {
     if (hipStreamSynchronize(sl[j]->st) != hipSuccess) rc = TBG_E_DEVICE;
@@ -533,13 +543,13 @@ int tbg_replay_multi(tbg_ctx* c, const tbg_ticket* tickets, uint32_t n_tickets, 
   if (rc == TBG_OK) {
     for (uint32_t k = 0; k < iters; ++k) {
       float m[8];
-      chain_times(ev.data() + 10ull * k, m);
+      chain_times(ev.data() + (size_t)kChainEvents * k, m);
       for (int j = 0; j < 7; ++j) acc[j] += m[j];
     }
     // wall time: first launch's start to the latest chain end
     for (uint32_t k = (iters > n_tickets ? iters - n_tickets : 0); k < iters; ++k) {
       float w = 0;
-      hipEventElapsedTime(&w, ev[0], ev[10ull * k + 9]);
+      hipEventElapsedTime(&w, ev[0], ev[(size_t)kChainEvents * k + 9]);
       if (w > acc[7]) acc[7] = w;
     }
     if (ms8) memcpy(ms8, acc, sizeof(acc));

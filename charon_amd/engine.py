@@ -69,11 +69,11 @@ class Engine:
     """One context = one GPU (HIP device ordinal)."""
 
     def __init__(self, device: int = 0, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0,
-                 rlc_seed: int = 0, rlc_chunk: int = 0):
+                 rlc_seed: int = 0, rlc_chunk: int = 0, streams_per_slot: int = 0):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
-                                rlc_chunk=rlc_chunk)
+                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot)
         h = ctypes.c_void_p()
         rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
         self._check(rc, "tbg_init")

@@ -80,7 +80,7 @@ typedef struct {
   uint32_t rlc_group;     /* duties per level-1 RLC group (0 -> 8)               */
   uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests) */
   uint32_t rlc_chunk;     /* duties per Miller-loop quad inside a group (0 -> 2)  */
-  uint32_t reserved;
+  uint32_t streams_per_slot; /* 1 (0 -> 1) or 2: hash_to_G2 on its own stream   */
 } tbg_config;
 
 /* Verification schedule.  Both give every partial the verdict of the exact
