@@ -30,7 +30,16 @@ sys.path.insert(0, ROOT)
 # default), and streams sharing a queue serialise.  It is read once, at HIP
 # initialisation, so it is set before anything touches the GPU (the Go host
 # process sets it in its environment).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+def _hw_queues(argv):
+    for i, a in enumerate(argv):
+        if a == "--hw-queues" and i + 1 < len(argv):
+            return argv[i + 1]
+        if a.startswith("--hw-queues="):
+            return a.split("=", 1)[1]
+    return "16"
+
+
+os.environ["GPU_MAX_HW_QUEUES"] = _hw_queues(sys.argv)
 
 METRIC = "verified+aggregated 3-of-4 threshold BLS sigs/sec at 1/2/4/8 MI355X"
 # Measured on MI355X by tools/microbench/valu_rates.hip (2 waves/SIMD, 8
@@ -118,6 +127,7 @@ def main():
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
+    ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (read at HIP init)")
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()

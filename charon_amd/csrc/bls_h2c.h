@@ -149,7 +149,11 @@ TBG_HD void hash_to_field_fp2(const uint8_t* msg, uint32_t msg_len, Fp2& u0, Fp2
   u1.c1 = fp_from_be64_mod(uni + 192);
 }
 
+TBG_NI G2J iso3_to_jac(const Fp2& x, const Fp2& y);
+
 // Simplified SWU to E2' then the 3-isogeny to E2, output Jacobian on E2.
+// Reference form (straight from RFC 9380 section 6.6.2); hash_to_g2 uses
+// map_to_curve_g2_pair below and falls back here only on exceptional inputs.
 TBG_NI G2J map_to_curve_g2(const Fp2& u) {
   Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B), Z = fp2_from_const(SSWU_Z);
   Fp2 u2 = fp2_sqr(u);
@@ -172,8 +176,13 @@ TBG_NI G2J map_to_curve_g2(const Fp2& u) {
     fp2_sqrt(gx2, y);  // always a square when gx1 is not
   }
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_reduce(fp2_neg(y));
-  // 3-isogeny: x = x_num / x_den, y = y' y_num / y_den, as Jacobian
-  // (X, Y, Z) = (x_num x_den y_den^2, y' y_num x_den^3 y_den^2, x_den y_den).
+  return iso3_to_jac(x, y);
+}
+
+// 3-isogeny E2' -> E2 of an affine point: x = x_num / x_den, y = y' y_num /
+// y_den, as Jacobian (X, Y, Z) = (x_num x_den y_den^2, y' y_num x_den^3 y_den^2,
+// x_den y_den).
+TBG_NI G2J iso3_to_jac(const Fp2& x, const Fp2& y) {
   Fp2 xx = fp2_sqr(x), xxx = fp2_mul(xx, x);
   Fp2 xnum = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_from_const(ISO_K13), xxx), fp2_mul(fp2_from_const(ISO_K12), xx)),
                                 fp2_add(fp2_mul(fp2_from_const(ISO_K11), x), fp2_from_const(ISO_K10))));
@@ -191,12 +200,78 @@ TBG_NI G2J map_to_curve_g2(const Fp2& u) {
   return r;
 }
 
+// Root of a or of Z a, whichever is a square (a non-square in Fp2 times the
+// non-square Z is a square), from one Fp exponentiation on the norm plus one
+// for the root (norm method, as fp2_sqrt).  sq reports which.  False on the
+// inputs the closed form does not cover (a.c1 == 0 or (Z a).c1 == 0), which
+// the caller routes to the reference path.
+TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) {
+  Fp2 a = fp2_reduce(a_in);
+  Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
+  Fp gamma = fp_pow_const<EXP_SQRT_BITS>(norm, EXP_SQRT_WORDS);
+  sq = fp_eq(fp_sqr(gamma), norm);
+  if (!sq) {
+    // gamma^2 = -norm(a); K gamma is a root of norm(Z) norm(a) = norm(Z a)
+    a = fp2_reduce(fp2_mul(fp2_from_const(SSWU_Z), a));
+    gamma = fp_mul(gamma, fp_from_const(SSWU_SQRT_NEG_NORM_Z));
+  }
+  if (fp_is_zero(a.c1)) return false;
+  Fp inv2 = fp_from_const(INV2_M);
+  Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);
+  Fp t = fp_pow_const<EXP_PM3D4_BITS>(delta, EXP_PM3D4_WORDS);  // delta^((p-3)/4)
+  Fp x0 = fp_mul(delta, t);
+  Fp h = fp_mul(fp_mul(a.c1, t), inv2);
+  bool res = fp_eq(fp_sqr(x0), delta);
+  Fp2 r = {fp_select(res, x0, h), fp_select(res, h, fp_reduce(fp_neg(x0)))};
+  root = r;
+  return fp2_eq(fp2_sqr(r), a);
+}
+
+// SSWU of both hash_to_field outputs with uniform control flow: one Fp2
+// inversion for the two denominators (Montgomery's trick) and one square
+// root per map -- when g(x1) is not a square, x2 = Z u^2 x1 and
+// g(x2) = Z^3 u^6 g(x1), so sqrt(g(x2)) = Z u^3 sqrt(Z g(x1)).
+// (The reference form tries sqrt(g(x1)), then sqrt(g(x2)): 1-2 roots and
+// an inversion per map, divergent across a wave.)
+TBG_NI void map_to_curve_g2_pair(const Fp2& u0, const Fp2& u1, G2J& q0, G2J& q1) {
+  const Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B), Z = fp2_from_const(SSWU_Z);
+  const Fp2* u[2] = {&u0, &u1};
+  Fp2 zu2[2], den[2];
+  for (int j = 0; j < 2; ++j) {
+    zu2[j] = fp2_reduce(fp2_mul(Z, fp2_sqr(*u[j])));
+    den[j] = fp2_reduce(fp2_add(fp2_sqr(zu2[j]), zu2[j]));
+  }
+  Fp2 dd = fp2_reduce(fp2_mul(den[0], den[1]));
+  bool ok = !fp2_is_zero(dd);
+  Fp2 di = fp2_inv(dd);
+  Fp2 inv[2] = {fp2_mul(den[1], di), fp2_mul(den[0], di)};
+  G2J* out[2] = {&q0, &q1};
+  for (int j = 0; j < 2 && ok; ++j) {
+    Fp2 x1 = fp2_mul(fp2_from_const(SSWU_NEG_B_OVER_A), fp2_reduce(fp2_add(fp2_one(), inv[j])));
+    Fp2 gx1 = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_sqr(x1), x1), fp2_mul(A, x1)), B));
+    Fp2 r;
+    bool sq;
+    if (!fp2_sqrt_or_z(gx1, r, sq)) {
+      ok = false;
+      break;
+    }
+    Fp2 x = sq ? x1 : fp2_mul(zu2[j], x1);
+    Fp2 y = sq ? r : fp2_mul(fp2_mul(Z, fp2_mul(fp2_sqr(*u[j]), *u[j])), r);
+    if (fp2_sgn0(*u[j]) != fp2_sgn0(y)) y = fp2_reduce(fp2_neg(y));
+    *out[j] = iso3_to_jac(x, y);
+  }
+  if (!ok) {  // exceptional inputs (probability ~2^-380 per hash): reference path
+    q0 = map_to_curve_g2(u0);
+    q1 = map_to_curve_g2(u1);
+  }
+}
+
 // H(m) in G2 (Jacobian).
 TBG_NI G2J hash_to_g2(const uint8_t* msg, uint32_t msg_len) {
   Fp2 u0, u1;
   hash_to_field_fp2(msg, msg_len, u0, u1);
-  G2J q0 = map_to_curve_g2(u0);
-  G2J q1 = map_to_curve_g2(u1);
+  G2J q0, q1;
+  map_to_curve_g2_pair(u0, u1, q0, q1);
   return g2_clear_cofactor(jac_add(q0, q1));
 }
 

@@ -25,29 +25,9 @@
 #include "bls_h2c.h"
 #include "bls_lines.h"
 #include "bls_quad.h"
+#include "bls_rlc.h"
 
 namespace tbg {
-
-// r_i: 64 bits of SHA-256's compression function keyed by the batch seed.
-TBG_HD uint64_t rlc_scalar(const uint32_t (&seed)[8], uint32_t i) {
-  uint8_t blk[64];
-  for (int k = 0; k < 8; ++k) {
-    blk[4 * k] = (uint8_t)(seed[k] >> 24);
-    blk[4 * k + 1] = (uint8_t)(seed[k] >> 16);
-    blk[4 * k + 2] = (uint8_t)(seed[k] >> 8);
-    blk[4 * k + 3] = (uint8_t)seed[k];
-  }
-  for (int k = 32; k < 64; ++k) blk[k] = 0;
-  blk[32] = (uint8_t)(i >> 24);
-  blk[33] = (uint8_t)(i >> 16);
-  blk[34] = (uint8_t)(i >> 8);
-  blk[35] = (uint8_t)i;
-  blk[36] = 0x80;
-  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au, 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-  sha256_block(h, blk);
-  uint64_t r = ((uint64_t)h[0] << 32) | h[1];
-  return r ? r : 1;
-}
 
 // Candidate = decoded fine with a usable public key.  k_rlc_partial turns
 // non-candidates' NOT_VERIFIED into ERR_PUBKEY concurrently, so the test reads
@@ -62,20 +42,9 @@ __device__ __forceinline__ bool rlc_candidate(const DevBatch& B, uint32_t i) {
   return B.partial_status[i] == TBG_PS_NOT_VERIFIED;
 }
 
-TBG_HD G2A g2_psi_aff(const G2A& a) {
-  return {fp2_mul(fp2_conj(a.x), fp2_from_const(PSI_X)), fp2_mul(fp2_conj(a.y), fp2_from_const(PSI_Y))};
-}
-
 // ------------------------------------------------------------------ level 0
-// One thread per partial: r_i s_i and r_i pk_i.  The 64 random bits are four
-// 16-bit digits a_k of r_i = a_0 + a_1 x + a_2 x^2 + a_3 x^3 (x the curve
-// parameter; distinct digit vectors give distinct r_i mod r because
-// 2^16 < |x| and 2^16 |x|^3 < r, so a false accept stays <= 2^-64).  The
-// subgroup check already proved psi(s) = [x] s for every decoded signature,
-// and on G1 [x^2] = -phi, so
-//   r_i s_i  = sum_k a_k psi^k(s_i)
-//   r_i pk_i = a_0 pk + a_1 [x]pk - a_2 phi(pk) - a_3 phi([x]pk)
-// are 16-bit four-point Straus products ([x]pk is resident in the key table).
+// One thread per partial: [r_i] s_i and [r_i] pk_i by the base-x digit
+// method of bls_rlc.h (four-point, 16-bit Straus products).
 __global__ void __launch_bounds__(64) k_rlc_partial(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
                                                     const int32_t* pk_status, uint32_t n_pk) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -97,37 +66,10 @@ __global__ void __launch_bounds__(64) k_rlc_partial(DevBatch B, const G1A* pk_af
     B.part_p[i] = jac_from_aff(p0);
     return;
   }
-  uint64_t r = rlc_scalar(B.rlc_seed, i);
-  uint32_t a[4] = {(uint32_t)(r & 0xFFFF), (uint32_t)((r >> 16) & 0xFFFF), (uint32_t)((r >> 32) & 0xFFFF),
-                   (uint32_t)(r >> 48)};
-  G2A sq[4];
-  sq[0] = s0;
-  sq[1] = g2_psi_aff(sq[0]);
-  sq[2] = g2_psi_aff(sq[1]);
-  sq[3] = g2_psi_aff(sq[2]);
-  const G1A p1 = xpk_aff[pid];
-  const Fp beta = fp_from_const(G1_BETA);
-  G1A pq[4];
-  pq[0] = p0;
-  pq[1] = p1;
-  pq[2] = {fp_mul(p0.x, beta), fp_reduce(fp_neg(p0.y))};
-  pq[3] = {fp_mul(p1.x, beta), fp_reduce(fp_neg(p1.y))};
-  G2J S = jac_inf<Fp2>();
-  G1J P = jac_inf<Fp>();
-  bool started = false;
-  for (int bit = 15; bit >= 0; --bit) {
-    if (started) {
-      S = jac_dbl(S);
-      P = jac_dbl(P);
-    }
-    for (int k = 0; k < 4; ++k) {
-      if ((a[k] >> bit) & 1) {
-        S = jac_add_aff(S, sq[k]);
-        P = jac_add_aff(P, pq[k]);
-        started = true;
-      }
-    }
-  }
+  uint32_t a[4];
+  rlc_digits(rlc_scalar(B.rlc_seed, i), a);
+  G2J S = rlc_mul_g2(s0, a);
+  G1J P = rlc_mul_g1(p0, xpk_aff[pid], a);
   B.part_s[i] = S;
   B.part_p[i] = P;
 }
@@ -187,10 +129,21 @@ __global__ void __launch_bounds__(64) k_rlc_group_lines(DevBatch B) {
   B.grp_state[g] = GRP_LINES;
 }
 
-// f *= line(H(m) lines at step idx) evaluated at affine P = (-x, y).
+// f *= line(H(m) lines at step idx) evaluated at affine P = (-x, y).  The
+// two evaluation products are split over the quad (lane 0: l1 (-x), lane 1:
+// l4 y) and broadcast, instead of every lane computing both.
 __device__ __forceinline__ Fp4 quad_line_at(const Fp4& f, const uint32_t* lines, int idx, const Fp& nx, const Fp& y) {
-  Line h = line_load(lines + LINE_WORDS * idx);
-  return quad_line(f, h.l0, fp2_mul_fp(h.l1, nx), fp2_mul_fp(h.l4, y));
+  const uint32_t* src = lines + LINE_WORDS * idx;
+  const bool first = (threadIdx.x & 3) == 0;
+  Fp2 l0, lk;
+  for (int i = 0; i < NL; ++i) {
+    l0.c0.l[i] = src[i];
+    l0.c1.l[i] = src[NL + i];
+    lk.c0.l[i] = first ? src[2 * NL + i] : src[4 * NL + i];
+    lk.c1.l[i] = first ? src[3 * NL + i] : src[5 * NL + i];
+  }
+  Fp2 e = fp2_mul_fp(lk, first ? nx : y);
+  return quad_line(f, l0, xch<QP_B0>(e), xch<QP_B1>(e));
 }
 __device__ __forceinline__ Fp4 quad_line_folded(const Fp4& f, const uint32_t* lines, int idx) {
   Line a = line_load(lines + LINE_WORDS * idx);

@@ -337,3 +337,122 @@ int hc_stage_verify_quad(const uint8_t* pk48) {
   return fp12_is_one(r) ? 1 : 0;
 }
 }
+
+#include "../../charon_amd/csrc/bls_rlc.h"
+// RLC scalar application (k_rlc_partial) against plain scalar multiplication,
+// and per-stage operation counts of the RLC schedule (tools/count_work.py).
+extern "C" {
+static G1A hc_xpk(const G1A& pk) {
+  G1A x;
+  jac_to_aff(jac_neg(jac_mul_xabs(jac_from_aff(pk))), x);
+  return x;
+}
+// r_words: the scalar sum a_k x^k mod r as 8 little-endian u32 words.
+int hc_rlc_check(const uint8_t* sig96, const uint8_t* pk48, uint64_t r64, const uint32_t* r_words) {
+  G2A s;
+  G1A pk;
+  if (g2_decompress(sig96, s) != DEC_OK || g1_decompress(pk48, pk) != DEC_OK) return -1;
+  uint32_t a[4];
+  rlc_digits(r64, a);
+  G2J S = rlc_mul_g2(s, a);
+  G1J P = rlc_mul_g1(pk, hc_xpk(pk), a);
+  G2J S_ref = jac_mul_words(jac_from_aff(s), r_words, 255);
+  G1J P_ref = jac_mul_words(jac_from_aff(pk), r_words, 255);
+  return (jac_eq(S, S_ref) ? 1 : 0) | (jac_eq(P, P_ref) ? 2 : 0);
+}
+uint64_t hc_rlc_scalar(const uint8_t* seed32, uint32_t i) {
+  uint32_t seed[8];
+  for (int k = 0; k < 8; ++k)
+    seed[k] = ((uint32_t)seed32[4 * k] << 24) | ((uint32_t)seed32[4 * k + 1] << 16) | ((uint32_t)seed32[4 * k + 2] << 8) | seed32[4 * k + 3];
+  return rlc_scalar(seed, i);
+}
+
+static G2A g_sig;
+static G1A g_pk, g_xpk;
+static G2A g_h;
+int hc_stage_setup(const uint8_t* sig96, const uint8_t* pk48, const uint8_t* msg, uint32_t len) {
+  if (g2_decompress(sig96, g_sig) != DEC_OK || g1_decompress(pk48, g_pk) != DEC_OK) return -1;
+  g_xpk = hc_xpk(g_pk);
+  jac_to_aff(hash_to_g2(msg, len), g_h);
+  return 0;
+}
+// one non-lead partial of k_rlc_partial (PRF + both digit products)
+void hc_stage_rlc_partial(uint64_t r64) {
+  uint32_t a[4];
+  rlc_digits(r64, a);
+  G2J S = rlc_mul_g2(g_sig, a);
+  G1J P = rlc_mul_g1(g_pk, g_xpk, a);
+  (void)S;
+  (void)P;
+}
+// k_rlc_duty_sum for n partials: n-1 Jacobian additions per group + G1 affine
+void hc_stage_duty_sum(int n) {
+  G1J P = jac_from_aff(g_pk), P1 = jac_dbl(P);
+  G2J S = jac_from_aff(g_sig), S1 = jac_dbl(S);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  G1J accP = P;
+  G2J accS = S;
+  for (int k = 1; k < n; ++k) {
+    accP = jac_add(accP, P1);
+    accS = jac_add(accS, S1);
+  }
+  G1A a;
+  jac_to_aff(accP, a);
+}
+// k_rlc_group_lines for G duties
+void hc_stage_group_lines(int G) {
+  G2J S = jac_from_aff(g_sig), S1 = jac_dbl(S);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  G2J acc = S;
+  for (int k = 1; k < G; ++k) acc = jac_add(acc, S1);
+  G2A a;
+  jac_to_aff(acc, a);
+  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  g2_lines(a, nx, fp_from_const(G1_NEG_Y), g_sig_lines);
+}
+// one k_rlc_miller_chunks quad: `pairs` duty pairs (+ the folded S pair)
+void hc_stage_miller_chunk(int pairs, int with_folded) {
+  Fp nx0 = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  g2_lines(g_sig, nx0, fp_from_const(G1_NEG_Y), g_sig_lines);
+  g2_lines(g_h, fp_one(), fp_one(), g_h_lines);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  qe::Q3 f;
+  f.v[0] = {fp2_one(), fp2_zero()};
+  f.v[1] = fp4_zero();
+  f.v[2] = fp4_zero();
+  int idx = 0;
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = qe::sqr(f);
+    int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+    for (int s = 0; s < steps; ++s, ++idx) {
+      if (with_folded) {
+        Line a = line_load(g_sig_lines + LINE_WORDS * idx);
+        f = qe::line(f, a.l0, a.l1, a.l4);
+      }
+      for (int k = 0; k < pairs; ++k) {
+        Line h = line_load(g_h_lines + LINE_WORDS * idx);
+        Fp nx = fp_reduce(fp_neg(g_pk.x));
+        // lanes 0 / 1 evaluate l1 (-x) / l4 y; lane 2 repeats lane 1's product
+        Fp2 e1 = fp2_mul_fp(h.l1, nx), e4 = fp2_mul_fp(h.l4, g_pk.y);
+        (void)fp2_mul_fp(h.l4, g_pk.y);
+        f = qe::line(f, h.l0, e1, e4);
+      }
+    }
+  }
+}
+// one k_rlc_group_final quad: nch - 1 products and the final exponentiation
+void hc_stage_group_final(int nch) {
+  qe::Q3 f;
+  f.v[0] = {fp2_one(), fp2_one()};
+  f.v[1] = {fp2_one(), fp2_zero()};
+  f.v[2] = fp4_zero();
+  for (int c = 1; c < nch; ++c) f = qe::mul(f, f);
+  f = qe::final_exp(qe::conj(f));
+}
+}

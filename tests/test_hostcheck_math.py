@@ -170,7 +170,11 @@ def test_g2_decompress_rejects_off_curve_and_non_subgroup():
 
 
 def test_hash_to_g2_matches_oracle():
-    for msg in [b"", b"abc", bytes(32), bytes(range(32)), b"Hello Obol", bytes(range(200))]:
+    # 30 messages = 60 SSWU maps: both the square and the non-square branch of
+    # map_to_curve_g2_pair are taken many times
+    msgs = [b"", b"abc", bytes(32), bytes(range(32)), b"Hello Obol", bytes(range(200))]
+    msgs += [bytes([i]) * (i + 1) for i in range(24)]
+    for msg in msgs:
         h = call("hc_hash_to_g2", msg, len(msg), out=96)
         assert h == bls.g2_compress(bls.hash_to_g2(msg))
 
@@ -253,3 +257,30 @@ def test_quad_verify_pipeline_emulated():
     bad[3] ^= 8
     assert lib().hc_stage_lines(bytes.fromhex(sig_hex), bytes(bad), len(bad)) == 0
     assert lib().hc_stage_verify_quad(bytes.fromhex(pk_hex)) == 0                 # wrong message
+
+
+def test_rlc_digit_scalars_match_plain_scalar_multiplication():
+    """k_rlc_partial applies r = a0 + a1 x + a2 x^2 + a3 x^3 through psi on G2
+    and phi / [x]pk on G1; both must equal [r mod order] P."""
+    import ctypes
+    L = lib()
+    L.hc_rlc_check.restype = ctypes.c_int
+    L.hc_rlc_check.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+    x = -bls.X_ABS
+    for trial in range(6):
+        sk = rng.randrange(1, bls.R)
+        msg = bytes([trial]) * 32
+        sig = bls.g2_compress(tb.sign(sk, msg))
+        pk = bls.g1_compress(tb.sk_to_pk(sk))
+        r64 = rng.getrandbits(64) if trial else 0xFFFF_FFFF_FFFF_FFFF
+        a = [(r64 >> (16 * k)) & 0xFFFF for k in range(4)]
+        r = sum(a[k] * x ** k for k in range(4)) % bls.R
+        words = (ctypes.c_uint32 * 8)(*[(r >> (32 * k)) & 0xFFFFFFFF for k in range(8)])
+        assert L.hc_rlc_check(sig, pk, r64, words) == 3
+
+
+def test_rlc_digit_scalars_are_distinct_mod_r():
+    """Distinct digit vectors give distinct scalars (the 2^-64 soundness bound):
+    |x| > 2^16 and 2^16 |x|^3 < r, checked on the extreme digit values."""
+    x = bls.X_ABS
+    assert (1 << 16) < x and (1 << 16) * x ** 3 < bls.R
