@@ -63,12 +63,44 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     jobs = jobs or min(len(units), max(1, (os.cpu_count() or 4)), 8)
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_unit, units))
+    for obj in objs:
+        check_return_address(obj)
     cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", target + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(target + ".tmp", target)
     return target
+
+
+def check_return_address(obj: str) -> None:
+    """Refuse a code object in which a callable function clobbers its return
+    address.  When a loop body in an out-of-line device function exceeds the
+    16-bit branch range, this compiler expands the long branch as
+    `s_getpc_b64 s[30:31]` ... `s_setpc_b64 s[30:31]` -- s[30:31] holds the
+    function's return address, so the return jumps into the function again
+    and the kernel never finishes (observed on gfx950).  Kernels use a free
+    SGPR pair and are not affected."""
+    llvm = "/opt/rocm/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-objdump")):
+        return
+    import re
+    import tempfile
+    heads = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-h", obj], capture_output=True, text=True).stdout
+    if ".hip_fatbin" not in heads:
+        return  # host-only translation unit
+    with tempfile.TemporaryDirectory() as td:
+        fat, co = os.path.join(td, "fatbin"), os.path.join(td, "co")
+        subprocess.check_call([os.path.join(llvm, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", obj,
+                               os.path.join(td, "stripped.o")])
+        subprocess.check_call([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", f"--input={fat}", "--type=o",
+                               "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"])
+        asm = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", co], capture_output=True, text=True,
+                             check=True).stdout
+    bad = len(re.findall(r"s_getpc_b64\s+s\[30:31\]", asm))
+    if bad:
+        raise RuntimeError(f"{obj}: {bad} long branch(es) through s[30:31] in an out-of-line function "
+                           "(return-address clobber; would hang on the GPU) -- keep that loop body smaller")
 
 
 class TbgBatch(ctypes.Structure):

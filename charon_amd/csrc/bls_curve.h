@@ -52,7 +52,7 @@ template <class F> TBG_HD Jac<F> jac_from_aff(const Aff<F>& a) { return {a.x, a.
 template <class F> TBG_HD Jac<F> jac_neg(const Jac<F>& p) { return {p.X, f_reduce(f_neg(p.Y)), p.Z}; }
 
 // dbl-2009-l (a = 0). Inputs < 2p, outputs < 2p.
-template <class F> TBG_NI Jac<F> jac_dbl(const Jac<F>& p) {
+template <class F> TBG_PT Jac<F> jac_dbl(const Jac<F>& p) {
   F A = f_sqr(p.X);
   F B = f_sqr(p.Y);
   F C = f_sqr(B);
@@ -68,7 +68,7 @@ template <class F> TBG_NI Jac<F> jac_dbl(const Jac<F>& p) {
 }
 
 // add-2007-bl with the exceptional cases handled (P == Q, P == -Q, infinity).
-template <class F> TBG_NI Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+template <class F> TBG_PT Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = f_sqr(p.Z);
@@ -96,7 +96,7 @@ template <class F> TBG_NI Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // Mixed addition P (Jacobian) + Q (affine), exceptional cases handled.
-template <class F> TBG_NI Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
+template <class F> TBG_PT Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.Z);
   F U2 = f_mul(q.x, Z1Z1);

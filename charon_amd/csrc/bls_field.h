@@ -23,10 +23,37 @@
 #define TBG_HD __host__ __device__ __forceinline__
 // Out-of-line on the device: shared code for the big tower/curve routines
 // keeps kernels within the instruction cache and compile times sane.
+// Out-of-line device functions.  Calls pass the large point / tower structs
+// through the scratch stack, but inlining whole call trees into the kernels
+// (-DTBG_INLINE_ALL=1) costs 15+ min of compile time, drops every kernel to
+// one wave per SIMD (AGPR spill space) and spills thousands of VGPRs in the
+// final exponentiation; and inlining only the point / quad primitives
+// (TBG_INLINE_PT=1) must not be combined with an out-of-line caller whose
+// loop body then exceeds the branch range: this compiler expands such long
+// branches through s[30:31], the caller's return address (a hang on gfx950).
+#if defined(TBG_INLINE_ALL) && TBG_INLINE_ALL
+#define TBG_NI __host__ __device__ __forceinline__
+#else
 #define TBG_NI __host__ __device__ __noinline__ inline
+#endif
+// Point / line / quad primitives: out of line unless TBG_INLINE_PT=1 or
+// TBG_INLINE_ALL=1 (see above).
+#ifndef TBG_INLINE_PT
+#if defined(TBG_INLINE_ALL) && TBG_INLINE_ALL
+#define TBG_INLINE_PT 1
+#else
+#define TBG_INLINE_PT 0
+#endif
+#endif
+#if TBG_INLINE_PT
+#define TBG_PT __host__ __device__ __forceinline__
+#else
+#define TBG_PT __host__ __device__ __noinline__ inline
+#endif
 #else
 #define TBG_HD inline
 #define TBG_NI inline
+#define TBG_PT inline
 #endif
 
 #if defined(TBG_BOUNDS_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
@@ -158,6 +185,22 @@ TBG_HD Fp fp_canon(const Fp& a) { return fp_csub_p(fp_reduce(a)); }
 // 64-bit accumulators and the m*p products over two, so consecutive
 // v_mad_u64_u32 never depend on each other; only the m_k / carry chain is
 // serial from column to column.
+#ifndef TBG_ACC_AB
+#define TBG_ACC_AB 4  // independent 64-bit accumulators for the a*b products of a column
+#endif
+#ifndef TBG_ACC_MP
+#define TBG_ACC_MP 2  // ... and for the m*p products
+#endif
+static_assert(TBG_ACC_AB == 1 || TBG_ACC_AB == 2 || TBG_ACC_AB == 4, "TBG_ACC_AB");
+static_assert(TBG_ACC_MP == 1 || TBG_ACC_MP == 2, "TBG_ACC_MP");
+
+template <int N>
+TBG_HD uint64_t acc_total(const uint64_t (&s)[N]) {
+  if constexpr (N == 4) return (s[0] + s[1]) + (s[2] + s[3]);
+  else if constexpr (N == 2) return s[0] + s[1];
+  else return s[0];
+}
+
 template <int K>
 TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
   TBG_COUNT(196 * (K + 1));
@@ -166,8 +209,8 @@ TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * NL - 1; ++k) {
-    uint64_t s[4] = {0, 0, 0, 0};
-    uint64_t t[2] = {0, 0};
+    uint64_t s[TBG_ACC_AB] = {};
+    uint64_t t[TBG_ACC_MP] = {};
     int c = 0;
     const int lo = k < NL ? 0 : k - NL + 1;
     const int hi = k < NL ? k : NL - 1;
@@ -175,14 +218,14 @@ TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
     for (int i = lo; i <= hi; ++i) {
 #pragma unroll
       for (int n = 0; n < K; ++n) {
-        s[c & 3] += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
+        s[c % TBG_ACC_AB] += (uint64_t)a[n]->l[i] * b[n]->l[k - i];
         ++c;
       }
     }
     const int mhi = k < NL ? k - 1 : NL - 1;
 #pragma unroll
-    for (int i = lo; i <= mhi; ++i) t[i & 1] += (uint64_t)m[i] * P_L[k - i];
-    uint64_t sum = ((s[0] + s[1]) + (s[2] + s[3])) + ((t[0] + t[1]) + acc);
+    for (int i = lo; i <= mhi; ++i) t[i % TBG_ACC_MP] += (uint64_t)m[i] * P_L[k - i];
+    uint64_t sum = acc_total(s) + (acc_total(t) + acc);
     if (k < NL) {
       m[k] = ((uint32_t)sum * NINV) & LMASK;
       sum += (uint64_t)m[k] * P_L[0];
@@ -223,20 +266,20 @@ TBG_HD Fp fp_sqr(const Fp& a) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * NL - 1; ++k) {
-    uint64_t s[4] = {0, 0, 0, 0};
-    uint64_t t[2] = {0, 0};
+    uint64_t s[TBG_ACC_AB] = {};
+    uint64_t t[TBG_ACC_MP] = {};
     int c = 0;
     const int lo = k < NL ? 0 : k - NL + 1;
 #pragma unroll
     for (int i = lo; 2 * i < k; ++i) {
-      s[c & 3] += (uint64_t)a.l[i] * a2[k - i];
+      s[c % TBG_ACC_AB] += (uint64_t)a.l[i] * a2[k - i];
       ++c;
     }
-    if ((k & 1) == 0) s[c & 3] += (uint64_t)a.l[k / 2] * a.l[k / 2];
+    if ((k & 1) == 0) s[c % TBG_ACC_AB] += (uint64_t)a.l[k / 2] * a.l[k / 2];
     const int mhi = k < NL ? k - 1 : NL - 1;
 #pragma unroll
-    for (int i = lo; i <= mhi; ++i) t[i & 1] += (uint64_t)m[i] * P_L[k - i];
-    uint64_t sum = ((s[0] + s[1]) + (s[2] + s[3])) + ((t[0] + t[1]) + acc);
+    for (int i = lo; i <= mhi; ++i) t[i % TBG_ACC_MP] += (uint64_t)m[i] * P_L[k - i];
+    uint64_t sum = acc_total(s) + (acc_total(t) + acc);
     if (k < NL) {
       m[k] = ((uint32_t)sum * NINV) & LMASK;
       sum += (uint64_t)m[k] * P_L[0];

@@ -32,7 +32,7 @@ TBG_HD Line line_load(const uint32_t* src) {
 
 // All 68 lines of Q in loop order; nxP / yP = (-x_P, y_P) to fold P in, or
 // (1, 1) (Montgomery one) to leave it out.
-TBG_NI void g2_lines(const G2A& Q, const Fp& nxP, const Fp& yP, uint32_t* out) {
+TBG_PT void g2_lines(const G2A& Q, const Fp& nxP, const Fp& yP, uint32_t* out) {
   G2J T = jac_from_aff(Q);
   int idx = 0;
   for (int i = 62; i >= 0; --i) {

@@ -118,6 +118,14 @@ TBG_HD Fp12 quad_to_fp12(const Fp4& A0, const Fp4& A1, const Fp4& A2) {
 namespace tbg {
 
 #define TBG_DEV __device__ __forceinline__
+#ifndef TBG_INLINE_QUAD
+#define TBG_INLINE_QUAD TBG_INLINE_PT
+#endif
+#if TBG_INLINE_QUAD
+#define TBG_QUAD_FN __forceinline__
+#else
+#define TBG_QUAD_FN __noinline__
+#endif
 
 // quad_perm controls (lane q reads lane sel[q]); lane 3 behaves as lane 2.
 constexpr int QP_NEXT = 1 | (2 << 2) | (0 << 4) | (0 << 6);  // (q + 1) mod 3
@@ -147,7 +155,7 @@ TBG_DEV int quad_lane() {
 }
 
 // C = A * B (both quad-distributed)
-__device__ __noinline__ Fp4 quad_mul(const Fp4& A, const Fp4& B) {
+__device__ TBG_QUAD_FN Fp4 quad_mul(const Fp4& A, const Fp4& B) {
   int q = quad_lane();
   Fp4 SA = fp4_add(xch<QP_NEXT>(A), xch<QP_PREV>(A));
   Fp4 SB = fp4_add(xch<QP_NEXT>(B), xch<QP_PREV>(B));
@@ -156,7 +164,7 @@ __device__ __noinline__ Fp4 quad_mul(const Fp4& A, const Fp4& B) {
   return quad_combine(q, P, xch<QP_NEXT>(P), xch<QP_PREV>(P), xch<QP_SW12>(Q));
 }
 
-__device__ __noinline__ Fp4 quad_sqr(const Fp4& A) {
+__device__ TBG_QUAD_FN Fp4 quad_sqr(const Fp4& A) {
   int q = quad_lane();
   Fp4 SA = fp4_add(xch<QP_NEXT>(A), xch<QP_PREV>(A));
   Fp4 P = fp4_sqr(A);
@@ -164,12 +172,12 @@ __device__ __noinline__ Fp4 quad_sqr(const Fp4& A) {
   return quad_combine(q, P, xch<QP_NEXT>(P), xch<QP_PREV>(P), xch<QP_SW12>(Q));
 }
 
-__device__ __noinline__ Fp4 quad_cyc_sqr(const Fp4& A) {
+__device__ TBG_QUAD_FN Fp4 quad_cyc_sqr(const Fp4& A) {
   Fp4 T = fp4_sqr(A);
   return quad_cyc_lane(quad_lane(), A, xch<QP_SW12>(T));
 }
 
-__device__ __noinline__ Fp4 quad_line(const Fp4& A, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
+__device__ TBG_QUAD_FN Fp4 quad_line(const Fp4& A, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
   return quad_line_lane(quad_lane(), A, xch<QP_NEXT>(A), l0, l1, l4);
 }
 
@@ -186,10 +194,10 @@ TBG_DEV Fp4 quad_one() {
 TBG_DEV Fp12 quad_gather(const Fp4& A) { return quad_to_fp12(xch<QP_B0>(A), xch<QP_B1>(A), xch<QP_B2>(A)); }
 
 // f^-1 via the tower inverse, replicated on the lanes of the quad.
-__device__ __noinline__ Fp4 quad_inv(const Fp4& A) { return quad_from_fp12(quad_lane(), fp12_inv(quad_gather(A))); }
+__device__ TBG_QUAD_FN Fp4 quad_inv(const Fp4& A) { return quad_from_fp12(quad_lane(), fp12_inv(quad_gather(A))); }
 
 // a^|x| in the cyclotomic subgroup
-__device__ __noinline__ Fp4 quad_pow_xabs(const Fp4& a) {
+__device__ TBG_QUAD_FN Fp4 quad_pow_xabs(const Fp4& a) {
   Fp4 r = a;
   for (int i = 62; i >= 0; --i) {
     r = quad_cyc_sqr(r);
@@ -200,7 +208,7 @@ __device__ __noinline__ Fp4 quad_pow_xabs(const Fp4& a) {
 TBG_DEV Fp4 quad_pow_x(const Fp4& a) { return quad_conj(quad_pow_xabs(a)); }
 
 // f^(3 (p^12 - 1) / r), as final_exp() in bls_pairing.h.
-__device__ __noinline__ Fp4 quad_final_exp(const Fp4& f) {
+__device__ TBG_QUAD_FN Fp4 quad_final_exp(const Fp4& f) {
   Fp4 t = quad_mul(quad_conj(f), quad_inv(f));
   t = quad_mul(quad_frob(quad_frob(t)), t);
   Fp4 a = quad_mul(quad_pow_x(t), quad_conj(t));

@@ -5,7 +5,7 @@
 
 namespace tbg {
 
-__global__ void __launch_bounds__(64) k_lagrange(DevBatch B) {
+__global__ void TBG_LAUNCH k_lagrange(DevBatch B) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B.n_partials) return;
   uint32_t* w = B.lam + 8ull * i;
@@ -25,7 +25,7 @@ __global__ void __launch_bounds__(64) k_lagrange(DevBatch B) {
   for (int j = 0; j < 8; ++j) w[j] = lw[j];
 }
 
-__global__ void __launch_bounds__(64) k_aggregate(DevBatch B) {
+__global__ void TBG_LAUNCH k_aggregate(DevBatch B) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= B.n_duties) return;
   uint8_t* out = B.agg + 96ull * d;
@@ -75,10 +75,10 @@ __global__ void __launch_bounds__(64) k_aggregate(DevBatch B) {
 }
 
 void launch_lagrange(const DevBatch& B, hipStream_t st) {
-  if (B.n_partials) hipLaunchKernelGGL(k_lagrange, grid_for(B.n_partials), dim3(kBlock), 0, st, B);
+  if (B.n_partials) TBG_KLAUNCH(k_lagrange, grid_for(B.n_partials), dim3(kBlock), st, B);
 }
 void launch_aggregate(const DevBatch& B, hipStream_t st) {
-  if (B.n_duties) hipLaunchKernelGGL(k_aggregate, grid_for(B.n_duties), dim3(kBlock), 0, st, B);
+  if (B.n_duties) TBG_KLAUNCH(k_aggregate, grid_for(B.n_duties), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

@@ -8,7 +8,7 @@ namespace tbg {
 // Resident table entry: the key and [x]key (x the curve parameter), so the
 // RLC scalars of k_rlc.hip can be applied in base-x digits with the G1
 // endomorphism ([x^2] = -phi on G1) instead of 64-bit double-and-add.
-__global__ void __launch_bounds__(64) k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x,
+__global__ void TBG_LAUNCH k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x,
                                                        int32_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(64) k_decode_pubkeys(const uint8_t* pk48, uint
   status[i] = st;
 }
 
-__global__ void __launch_bounds__(64) k_decode_sigs(DevBatch B) {
+__global__ void TBG_LAUNCH k_decode_sigs(DevBatch B) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B.n_partials) return;
   uint8_t b[96];
@@ -44,10 +44,10 @@ __global__ void __launch_bounds__(64) k_decode_sigs(DevBatch B) {
 }
 
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_decode_pubkeys, grid_for(n), dim3(kBlock), 0, st, pk48, n, out, out_x, status);
+  if (n) TBG_KLAUNCH(k_decode_pubkeys, grid_for(n), dim3(kBlock), st, pk48, n, out, out_x, status);
 }
 void launch_decode_sigs(const DevBatch& B, hipStream_t st) {
-  if (B.n_partials) hipLaunchKernelGGL(k_decode_sigs, grid_for(B.n_partials), dim3(kBlock), 0, st, B);
+  if (B.n_partials) TBG_KLAUNCH(k_decode_sigs, grid_for(B.n_partials), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

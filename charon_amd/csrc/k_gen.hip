@@ -44,11 +44,11 @@ __global__ void __launch_bounds__(64) k_sign(const uint8_t* sk32, const uint32_t
 }
 
 void launch_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* pk48, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_sk_to_pk, grid_for(n), dim3(kBlock), 0, st, sk32, n, pk48);
+  if (n) TBG_KLAUNCH(k_sk_to_pk, grid_for(n), dim3(kBlock), st, sk32, n, pk48);
 }
 void launch_sign(const uint8_t* sk32, const uint32_t* item_msg, uint32_t n, const G2A* h_aff, const int32_t* h_status,
                  uint8_t* sig96, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_sign, grid_for(n), dim3(kBlock), 0, st, sk32, item_msg, n, h_aff, h_status, sig96);
+  if (n) TBG_KLAUNCH(k_sign, grid_for(n), dim3(kBlock), st, sk32, item_msg, n, h_aff, h_status, sig96);
 }
 
 }  // namespace tbg

@@ -4,7 +4,7 @@
 
 namespace tbg {
 
-__global__ void __launch_bounds__(64) k_hash_msgs(DevBatch B) {
+__global__ void TBG_LAUNCH k_hash_msgs(DevBatch B) {
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= B.n_msgs) return;
   uint32_t off = B.msg_off[m], len = B.msg_off[m + 1] - off;
@@ -20,7 +20,7 @@ __global__ void __launch_bounds__(64) k_hash_msgs(DevBatch B) {
 }
 
 void launch_hash_msgs(const DevBatch& B, hipStream_t st) {
-  if (B.n_msgs) hipLaunchKernelGGL(k_hash_msgs, grid_for(B.n_msgs), dim3(kBlock), 0, st, B);
+  if (B.n_msgs) TBG_KLAUNCH(k_hash_msgs, grid_for(B.n_msgs), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

@@ -45,7 +45,7 @@ __device__ __forceinline__ bool rlc_candidate(const DevBatch& B, uint32_t i) {
 // ------------------------------------------------------------------ level 0
 // One thread per partial: [r_i] s_i and [r_i] pk_i by the base-x digit
 // method of bls_rlc.h (four-point, 16-bit Straus products).
-__global__ void __launch_bounds__(64) k_rlc_partial(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
+__global__ void TBG_LAUNCH k_rlc_partial(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
                                                     const int32_t* pk_status, uint32_t n_pk) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B.n_partials) return;
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(64) k_rlc_partial(DevBatch B, const G1A* pk_af
 }
 
 // One thread per duty: P_d = sum r_i pk_i (affine) and S_d = sum r_i s_i.
-__global__ void __launch_bounds__(64) k_rlc_duty_sum(DevBatch B) {
+__global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= B.n_duties) return;
   G1J P = jac_inf<Fp>();
@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(64) k_rlc_duty_sum(DevBatch B) {
 }
 
 // One thread per group: S = sum of the group's S_d, its Miller lines (-g1 folded in).
-__global__ void __launch_bounds__(64) k_rlc_group_lines(DevBatch B) {
+__global__ void TBG_LAUNCH k_rlc_group_lines(DevBatch B) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
@@ -171,7 +171,7 @@ __device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
 // Level 1, Miller part: one quad per (group, chunk of rlc_chunk duties); the
 // group's S pair rides in chunk 0.  Chunks share nothing but the final
 // exponentiation, so a group's pairs are spread over several quads.
-__global__ void __launch_bounds__(64) k_rlc_miller_chunks(DevBatch B) {
+__global__ void TBG_LAUNCH k_rlc_miller_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(64) k_rlc_miller_chunks(DevBatch B) {
 
 // Level 1, final part: one quad per group multiplies its chunks' products
 // and runs the one final exponentiation of the group.
-__global__ void __launch_bounds__(64) k_rlc_group_final(DevBatch B) {
+__global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
@@ -238,7 +238,7 @@ __device__ __forceinline__ void rlc_push_partials(const DevBatch& B, uint32_t d)
 }
 
 // After level 1 (one thread per duty): accept, split into level 2, or go to level 3.
-__global__ void __launch_bounds__(64) k_rlc_resolve_groups(DevBatch B) {
+__global__ void TBG_LAUNCH k_rlc_resolve_groups(DevBatch B) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= B.n_duties) return;
   int32_t st = B.dv_state[d];
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(64) k_rlc_resolve_groups(DevBatch B) {
 }
 
 // Level 2 lines: one thread per listed duty.
-__global__ void __launch_bounds__(64) k_rlc_duty_lines(DevBatch B) {
+__global__ void TBG_LAUNCH k_rlc_duty_lines(DevBatch B) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= B.counters[CNT_DUTIES]) return;
   uint32_t d = B.dv_list[k];
@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(64) k_rlc_duty_lines(DevBatch B) {
 }
 
 // Level 2 check: one quad per listed duty; failures go to level 3.
-__global__ void __launch_bounds__(64) k_rlc_check_duties(DevBatch B) {
+__global__ void TBG_LAUNCH k_rlc_check_duties(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t k = t >> 2;
   if (k >= B.counters[CNT_DUTIES]) return;
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(64) k_rlc_check_duties(DevBatch B) {
 }
 
 // Per-partial schedule (TBG_VERIFY_EACH): every candidate goes to level 3.
-__global__ void __launch_bounds__(64) k_list_all_partials(DevBatch B, const int32_t* pk_status, uint32_t n_pk) {
+__global__ void TBG_LAUNCH k_list_all_partials(DevBatch B, const int32_t* pk_status, uint32_t n_pk) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B.n_partials) return;
   if (!rlc_candidate(B, i)) return;
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(64) k_list_all_partials(DevBatch B, const int3
 }
 
 // Level 3 lines: one thread per listed partial, lines of its signature.
-__global__ void __launch_bounds__(64) k_lines_sig_list(DevBatch B) {
+__global__ void TBG_LAUNCH k_lines_sig_list(DevBatch B) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= B.counters[CNT_PARTIALS]) return;
   uint32_t i = B.part_list[k];
@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(64) k_lines_sig_list(DevBatch B) {
 }
 
 // Level 3 check: one quad per listed partial, the exact CoreVerify.
-__global__ void __launch_bounds__(64) k_verify_list(DevBatch B, const G1A* pk_aff) {
+__global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t k = t >> 2;
   if (k >= B.counters[CNT_PARTIALS]) return;
@@ -347,14 +347,14 @@ void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff
                         hipStream_t st) {
   if (!B.n_duties) return;
   if (B.rlc_group == 0) {
-    if (B.n_partials) hipLaunchKernelGGL(k_list_all_partials, grid_for(B.n_partials), dim3(kBlock), 0, st, B, pk_status, n_pk);
+    if (B.n_partials) TBG_KLAUNCH(k_list_all_partials, grid_for(B.n_partials), dim3(kBlock), st, B, pk_status, n_pk);
     return;
   }
   if (B.n_partials)
-    hipLaunchKernelGGL(k_rlc_partial, grid_for(B.n_partials), dim3(kBlock), 0, st, B, pk_aff, xpk_aff, pk_status, n_pk);
-  hipLaunchKernelGGL(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), 0, st, B);
+    TBG_KLAUNCH(k_rlc_partial, grid_for(B.n_partials), dim3(kBlock), st, B, pk_aff, xpk_aff, pk_status, n_pk);
+  TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B);
   uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
-  hipLaunchKernelGGL(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), 0, st, B);
+  TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
 }
 
 void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
@@ -362,17 +362,17 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
   if (B.rlc_group != 0) {
     uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
-    hipLaunchKernelGGL(k_rlc_miller_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), 0, st, B);
-    hipLaunchKernelGGL(k_rlc_group_final, grid_for(4 * n_groups), dim3(kBlock), 0, st, B);
-    hipLaunchKernelGGL(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), 0, st, B);
+    TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_rlc_group_final, grid_for(4 * n_groups), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
-      hipLaunchKernelGGL(k_rlc_duty_lines, grid_for(B.n_duties), dim3(kBlock), 0, st, B);
-      hipLaunchKernelGGL(k_rlc_check_duties, grid_for(4 * B.n_duties), dim3(kBlock), 0, st, B);
+      TBG_KLAUNCH(k_rlc_duty_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_check_duties, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
     }
   }
   if (B.n_partials) {
-    hipLaunchKernelGGL(k_lines_sig_list, grid_for(B.n_partials), dim3(kBlock), 0, st, B);
-    hipLaunchKernelGGL(k_verify_list, grid_for(4 * B.n_partials), dim3(kBlock), 0, st, B, pk_aff);
+    TBG_KLAUNCH(k_lines_sig_list, grid_for(B.n_partials), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_verify_list, grid_for(4 * B.n_partials), dim3(kBlock), st, B, pk_aff);
   }
 }
 

@@ -8,7 +8,7 @@
 
 namespace tbg {
 
-__global__ void __launch_bounds__(64) k_lines_h(DevBatch B) {
+__global__ void TBG_LAUNCH k_lines_h(DevBatch B) {
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= B.n_msgs) return;
   if (B.h_status[m] != 0) return;
@@ -16,7 +16,7 @@ __global__ void __launch_bounds__(64) k_lines_h(DevBatch B) {
 }
 
 void launch_h_lines(const DevBatch& B, hipStream_t st) {
-  if (B.n_msgs) hipLaunchKernelGGL(k_lines_h, grid_for(B.n_msgs), dim3(kBlock), 0, st, B);
+  if (B.n_msgs) TBG_KLAUNCH(k_lines_h, grid_for(B.n_msgs), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

@@ -18,6 +18,19 @@
 
 using namespace tbg;
 
+namespace tbg {
+void debug_after_launch(const char* kernel, hipStream_t st) {
+  static const bool on = getenv("TBG_DEBUG_SYNC") && getenv("TBG_DEBUG_SYNC")[0] == '1';
+  if (!on) return;
+  hipEvent_t a;
+  (void)hipEventCreate(&a);
+  (void)hipEventRecord(a, st);
+  hipError_t e = hipEventSynchronize(a);
+  (void)hipEventDestroy(a);
+  fprintf(stderr, "[tbg] %s done: %s\n", kernel, hipGetErrorString(e));
+}
+}  // namespace tbg
+
 namespace {
 
 constexpr int kChainEvents = 11;

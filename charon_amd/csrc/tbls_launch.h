@@ -10,6 +10,14 @@
 namespace tbg {
 
 constexpr int kBlock = 64;
+
+// Minimum waves per SIMD requested from the register allocator (1 lets a
+// kernel use all 512 / 2 = 256 VGPRs at two waves per SIMD; 3 caps it at
+// 168).  A tuning knob: tools/ab_variants.py builds -DTBG_MIN_WAVES=N.
+#ifndef TBG_MIN_WAVES
+#define TBG_MIN_WAVES 1
+#endif
+#define TBG_LAUNCH __launch_bounds__(64, TBG_MIN_WAVES)
 inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
 // Device-side layout of one batch (all pointers into device memory).
@@ -61,6 +69,16 @@ enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_WORDS = 4 };
 TBG_HD bool participates(uint32_t op, int32_t st) {
   return op == TBG_OP_VERIFY_AGGREGATE ? (st == TBG_PS_VALID) : (st == TBG_PS_NOT_VERIFIED);
 }
+
+// Debug aid: with TBG_DEBUG_SYNC=1 in the environment every launch is
+// followed by a stream synchronisation and a line on stderr (kernel, ms,
+// status), so a faulting or runaway kernel names itself.  Off by default.
+void debug_after_launch(const char* kernel, hipStream_t st);
+#define TBG_KLAUNCH(kernel, grid, block, st, ...)                      \
+  do {                                                                \
+    hipLaunchKernelGGL(kernel, grid, block, 0, st, __VA_ARGS__);      \
+    debug_after_launch(#kernel, st);                                  \
+  } while (0)
 
 // launchers (asynchronous on `st`)
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st);

@@ -23,7 +23,7 @@ def main():
     else:
         for so in sorted(glob.glob(os.path.join(ROOT, "variants", "*.so"))):
             env = dict(os.environ, TBG_LIB=so)
-            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "16", "--warmup", "1",
                                 "--no-cpu"], env=env, capture_output=True, text=True, timeout=600)
             try:
                 d = json.loads(r.stdout.strip().splitlines()[-1])

@@ -1,39 +1,22 @@
-"""CPU baseline for bench.py: the oracle (a CPU restatement of the reference
-tbls path, kind "port") timed on the host cores over a bounded sample of the
+"""CPU baseline for bench.py: the C restatement of the reference tbls path
+(oracle/c, kind "port") timed on the host cores over a bounded sample of the
 bench batch.  The reference Go/kryptology path cannot be built here (no Go
 toolchain, kryptology not vendored), so this is the labelled
 fallback of BASELINE.md.
 
-Per DV-duty the CPU does what the GPU step does: decode the n partial
-signatures (SigFromCore), H(m), n pairing checks, Lagrange combine, compress.
+Per DV-duty the CPU does what the reference does per tbls.VerifyAndAggregate
+call: decode the n partial signatures (SigFromCore, with subgroup checks),
+H(m), n two-pair pairing checks, Lagrange combination, compression.
 Pubshares are decoded once outside the timed region (startup in Charon,
-app/app.go:334-376).
+app/app.go:334-376).  One host thread per core, duties handed out
+dynamically (the reference runs one goroutine per peer message / duty).
 """
 from __future__ import annotations
 
 import os
 import time
-from concurrent.futures import ProcessPoolExecutor
 
-_STATE = {}
-
-
-def _init(pubshares_hex, t, n):
-    from oracle import bls12_381 as bls
-    _STATE["pk"] = [bls.g1_decompress(bytes.fromhex(h)) for h in pubshares_hex]
-    _STATE["t"], _STATE["n"] = t, n
-
-
-def _one(args):
-    from oracle import bls12_381 as bls
-    from oracle import tbls_oracle as tb
-    d, msg, sigs = args
-    n = _STATE["n"]
-    pks = _STATE["pk"][d * n:(d + 1) * n]
-    tss = tb.TSS({i + 1: pks[i] for i in range(n)}, n, _STATE["t"])
-    partials = [(i + 1, bls.g2_decompress(s)) for i, s in enumerate(sigs)]
-    agg, _ = tb.verify_and_aggregate(tss, partials, msg)
-    return bls.g2_compress(agg)
+import numpy as np
 
 
 def host_cores():
@@ -42,31 +25,32 @@ def host_cores():
     return max(1, min(n, cap))
 
 
-def run_cpu_baseline(batch, seconds: float = 15.0, max_dvs: int = 4096):
+def run_cpu_baseline(batch, seconds: float = 15.0, chunk: int = 512):
+    from oracle import c as oc
+    oc.build()
     cores = host_cores()
-    n_dv = min(batch.n_dv, max_dvs)
     n = batch.n
-    pks = [bytes(batch.pubshares[i]).hex() for i in range(n_dv * n)]
-    tasks = [(d, batch.msgs[d], [bytes(batch.sigs[d * n + i]) for i in range(n)]) for d in range(n_dv)]
-    done = 0
-    mismatches = 0
-    with ProcessPoolExecutor(max_workers=cores, initializer=_init, initargs=(pks, batch.t, n)) as ex:
-        # warm the workers (imports, pubshare decode) outside the timed region
-        list(ex.map(_init_probe, range(cores)))
-        t0 = time.perf_counter()
-        i = 0
-        while i < n_dv and time.perf_counter() - t0 < seconds:
-            chunk = tasks[i:i + cores]
-            for d_out, agg in zip(range(i, i + len(chunk)), ex.map(_one, chunk)):
-                mismatches += agg != bytes(batch.group_sig[d_out])
-            done += len(chunk)
-            i += len(chunk)
-        dt = time.perf_counter() - t0
+    table = oc.PubkeyTable(np.asarray(batch.pubshares, dtype=np.uint8))  # startup decode, untimed
+    first_id = int(batch.pubkey_ids[0])
+    done = mismatches = 0
+    t0 = time.perf_counter()
+    d0 = 0
+    while d0 < batch.n_dv and time.perf_counter() - t0 < seconds:
+        d1 = min(d0 + chunk, batch.n_dv)
+        nd = d1 - d0
+        sigs = np.asarray(batch.sigs[d0 * n:d1 * n], dtype=np.uint8)
+        ids = batch.identifiers[d0 * n:d1 * n]
+        pk_ids = (np.asarray(batch.pubkey_ids[d0 * n:d1 * n], dtype=np.int64) - first_id).astype(np.uint32)
+        msgs = np.asarray(batch.msg_data[d0 * 32:d1 * 32], dtype=np.uint8)
+        ps, ds, agg = oc.run(3, np.arange(nd + 1) * n, sigs, ids, table, msgs=msgs, msg_off=np.arange(nd + 1) * 32,
+                             duty_msg=np.arange(nd), pubkey_ids=pk_ids, duty_threshold=batch.threshold[d0:d1],
+                             threads=cores)
+        mismatches += int((ds != 0).sum()) + int((ps != 1).sum())
+        mismatches += int((agg != np.asarray(batch.group_sig[d0:d1])).any(axis=1).sum())
+        done += nd
+        d0 = d1
+    dt = time.perf_counter() - t0
     return {"value": round(done / dt, 3), "unit": "DV-duties/s", "cores": cores, "kind": "port",
-            "sample": f"first {done} DVs of the rank-0 bench batch ({batch.t}-of-{n}, Python oracle, "
-                      f"{cores} processes, {dt:.1f}s); CPU restatement, not the Go reference",
+            "sample": f"first {done} DVs of the rank-0 bench batch ({batch.t}-of-{n}); C restatement of the "
+                      f"reference per-item schedule (oracle/c), {cores} threads, {dt:.1f}s; not the Go reference",
             "mismatches": mismatches}
-
-
-def _init_probe(_):
-    return len(_STATE.get("pk", []))
