@@ -51,8 +51,10 @@ template <class F> TBG_HD bool jac_is_inf(const Jac<F>& p) { return f_is_zero(p.
 template <class F> TBG_HD Jac<F> jac_from_aff(const Aff<F>& a) { return {a.x, a.y, f_one<F>()}; }
 template <class F> TBG_HD Jac<F> jac_neg(const Jac<F>& p) { return {p.X, f_reduce(f_neg(p.Y)), p.Z}; }
 
+template <class F> TBG_NI Jac<F> jac_dbl(const Jac<F>& p);
+
 // dbl-2009-l (a = 0). Inputs < 2p, outputs < 2p.
-template <class F> TBG_PT Jac<F> jac_dbl(const Jac<F>& p) {
+template <class F> TBG_HD Jac<F> jac_dbl_in(const Jac<F>& p) {
   F A = f_sqr(p.X);
   F B = f_sqr(p.Y);
   F C = f_sqr(B);
@@ -68,7 +70,7 @@ template <class F> TBG_PT Jac<F> jac_dbl(const Jac<F>& p) {
 }
 
 // add-2007-bl with the exceptional cases handled (P == Q, P == -Q, infinity).
-template <class F> TBG_PT Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+template <class F> TBG_HD Jac<F> jac_add_in(const Jac<F>& p, const Jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = f_sqr(p.Z);
@@ -96,7 +98,7 @@ template <class F> TBG_PT Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // Mixed addition P (Jacobian) + Q (affine), exceptional cases handled.
-template <class F> TBG_PT Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
+template <class F> TBG_HD Jac<F> jac_add_aff_in(const Jac<F>& p, const Aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.Z);
   F U2 = f_mul(q.x, Z1Z1);
@@ -117,6 +119,13 @@ template <class F> TBG_PT Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   F Z3 = f_reduce(f_sub(f_sub(f_sqr(f_add(p.Z, H)), Z1Z1), HH));
   return {X3, Y3, Z3};
 }
+
+// Out-of-line forms (one copy of the code; struct arguments travel through
+// the scratch stack).  Kernels call the _in bodies from their own loops so
+// the operands stay in registers (see TBG_NI in bls_field.h).
+template <class F> TBG_NI Jac<F> jac_dbl(const Jac<F>& p) { return jac_dbl_in(p); }
+template <class F> TBG_NI Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) { return jac_add_in(p, q); }
+template <class F> TBG_NI Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) { return jac_add_aff_in(p, q); }
 
 template <class F> TBG_NI bool jac_to_aff(const Jac<F>& p, Aff<F>& out) {
   if (jac_is_inf(p)) return false;
@@ -159,6 +168,17 @@ template <class F> TBG_NI Jac<F> jac_mul_xabs(const Jac<F>& p) {
   return acc;
 }
 
+// Same schedule with the doublings inlined into the caller (call it from a
+// kernel body only: the loop body is ~90 KB of code, see bls_field.h).
+template <class F> TBG_HD Jac<F> jac_mul_xabs_in(const Jac<F>& p) {
+  Jac<F> acc = p;
+  for (int i = 62; i >= 0; --i) {
+    acc = jac_dbl_in(acc);
+    if ((X_ABS >> i) & 1) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+
 // [k] P for a multi-word scalar (little-endian 32-bit words, nbits significant).
 template <class F> TBG_NI Jac<F> jac_mul_words(const Jac<F>& p, const uint32_t* w, int nbits) {
   Jac<F> acc = jac_inf<F>();
@@ -180,6 +200,11 @@ TBG_HD G2J g2_psi(const G2J& p) {
 }
 
 // Subgroup membership for points on E2 (Scott 2021): P in G2 <=> psi(P) == [x] P.
+TBG_HD bool g2_in_subgroup_in(const G2J& p) {
+  if (jac_is_inf(p)) return true;
+  G2J xp = jac_neg(jac_mul_xabs_in(p));  // [x]P, x < 0
+  return jac_eq(g2_psi(p), xp);
+}
 TBG_NI bool g2_in_subgroup(const G2J& p) {
   if (jac_is_inf(p)) return true;
   G2J xp = jac_neg(jac_mul_xabs(p));  // [x]P, x < 0
@@ -194,17 +219,19 @@ TBG_HD bool g2_on_curve_aff(const G2A& a) {
 
 // Budroni-Pintore cofactor clearing (RFC 9380 G.3):
 //   h(P) = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P)
-TBG_NI G2J g2_clear_cofactor(const G2J& p) {
-  G2J t1 = jac_neg(jac_mul_xabs(p));         // [x]P
+template <bool INL>
+TBG_HD G2J g2_clear_cofactor_t(const G2J& p) {
+  G2J t1 = jac_neg(INL ? jac_mul_xabs_in(p) : jac_mul_xabs(p));   // [x]P
   G2J t2 = g2_psi(p);                         // psi(P)
   G2J t3 = g2_psi(g2_psi(jac_dbl(p)));        // psi^2(2P)
   t3 = jac_add(t3, jac_neg(t2));
   t2 = jac_add(t1, t2);
-  t2 = jac_neg(jac_mul_xabs(t2));             // [x](xP + psi P)
+  t2 = jac_neg(INL ? jac_mul_xabs_in(t2) : jac_mul_xabs(t2));     // [x](xP + psi P)
   t3 = jac_add(t3, t2);
   t3 = jac_add(t3, jac_neg(t1));
   return jac_add(t3, jac_neg(p));
 }
+TBG_NI G2J g2_clear_cofactor(const G2J& p) { return g2_clear_cofactor_t<false>(p); }
 
 // ------------------------------------------------------------------ G1 extra
 // P in G1 <=> phi(P) == -[x^2] P, phi(x, y) = (beta x, y).
@@ -225,8 +252,10 @@ enum DecodeStatus : int32_t {
   DEC_ERR_SUBGROUP = -4,
 };
 
-// 96-byte ZCash compressed G2 -> affine (Montgomery).
-TBG_NI int32_t g2_decompress(const uint8_t* b, G2A& out) {
+// 96-byte ZCash compressed G2 -> affine (Montgomery).  INL = true runs the
+// subgroup check's doublings inline (kernel callers).
+template <bool INL>
+TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out) {
   uint32_t c_flag = (b[0] >> 7) & 1, i_flag = (b[0] >> 6) & 1, s_flag = (b[0] >> 5) & 1;
   if (!c_flag) return DEC_ERR_FLAGS;
   uint8_t hi[48];
@@ -248,9 +277,10 @@ TBG_NI int32_t g2_decompress(const uint8_t* b, G2A& out) {
   if ((uint32_t)fp2_lex_largest(y) != s_flag) y = fp2_reduce(fp2_neg(y));
   out.x = x;
   out.y = y;
-  if (!g2_in_subgroup(jac_from_aff(out))) return DEC_ERR_SUBGROUP;
+  if (!(INL ? g2_in_subgroup_in(jac_from_aff(out)) : g2_in_subgroup(jac_from_aff(out)))) return DEC_ERR_SUBGROUP;
   return DEC_OK;
 }
+TBG_NI int32_t g2_decompress(const uint8_t* b, G2A& out) { return g2_decompress_t<false>(b, out); }
 
 // 48-byte ZCash compressed G1 -> affine (Montgomery).
 TBG_NI int32_t g1_decompress(const uint8_t* b, G1A& out) {

@@ -266,13 +266,16 @@ TBG_NI void map_to_curve_g2_pair(const Fp2& u0, const Fp2& u1, G2J& q0, G2J& q1)
   }
 }
 
-// H(m) in G2 (Jacobian).
-TBG_NI G2J hash_to_g2(const uint8_t* msg, uint32_t msg_len) {
+// H(m) in G2 (Jacobian).  INL = true inlines the cofactor clearing's
+// doublings (kernel callers only).
+template <bool INL>
+TBG_HD G2J hash_to_g2_t(const uint8_t* msg, uint32_t msg_len) {
   Fp2 u0, u1;
   hash_to_field_fp2(msg, msg_len, u0, u1);
   G2J q0, q1;
   map_to_curve_g2_pair(u0, u1, q0, q1);
-  return g2_clear_cofactor(jac_add(q0, q1));
+  return g2_clear_cofactor_t<INL>(jac_add(q0, q1));
 }
+TBG_NI G2J hash_to_g2(const uint8_t* msg, uint32_t msg_len) { return hash_to_g2_t<false>(msg, msg_len); }
 
 }  // namespace tbg

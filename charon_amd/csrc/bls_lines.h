@@ -31,14 +31,17 @@ TBG_HD Line line_load(const uint32_t* src) {
 }
 
 // All 68 lines of Q in loop order; nxP / yP = (-x_P, y_P) to fold P in, or
-// (1, 1) (Montgomery one) to leave it out.
-TBG_PT void g2_lines(const G2A& Q, const Fp& nxP, const Fp& yP, uint32_t* out) {
+// (1, 1) (Montgomery one) to leave it out.  INL = true inlines the doubling
+// and addition steps (kernel callers only: the loop body is ~100 KB).
+template <bool INL>
+TBG_HD void g2_lines_t(const G2A& Q, const Fp& nxP, const Fp& yP, uint32_t* out) {
   G2J T = jac_from_aff(Q);
   int idx = 0;
   for (int i = 62; i >= 0; --i) {
-    line_store(out + LINE_WORDS * idx++, miller_dbl(T, nxP, yP));
+    line_store(out + LINE_WORDS * idx++, INL ? miller_dbl_in(T, nxP, yP) : miller_dbl(T, nxP, yP));
     if ((X_ABS >> i) & 1) line_store(out + LINE_WORDS * idx++, miller_add(T, Q, nxP, yP));
   }
 }
+TBG_NI void g2_lines(const G2A& Q, const Fp& nxP, const Fp& yP, uint32_t* out) { g2_lines_t<false>(Q, nxP, yP, out); }
 
 }  // namespace tbg

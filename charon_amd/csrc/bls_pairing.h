@@ -14,7 +14,7 @@ namespace tbg {
 struct Line { Fp2 l0, l1, l4; };
 
 // T <- 2T; line through T tangent, evaluated at P (scaled by 2 Y Z^3 w^3).
-TBG_PT Line miller_dbl(G2J& T, const Fp& nxP, const Fp& yP) {
+TBG_HD Line miller_dbl_in(G2J& T, const Fp& nxP, const Fp& yP) {
   Fp2 A = fp2_sqr(T.X);
   Fp2 B = fp2_sqr(T.Y);
   Fp2 C = fp2_sqr(B);
@@ -36,7 +36,7 @@ TBG_PT Line miller_dbl(G2J& T, const Fp& nxP, const Fp& yP) {
 }
 
 // T <- T + Q (Q affine); line through T and Q evaluated at P (scaled by Z3 w^3).
-TBG_PT Line miller_add(G2J& T, const G2A& Q, const Fp& nxP, const Fp& yP) {
+TBG_HD Line miller_add_in(G2J& T, const G2A& Q, const Fp& nxP, const Fp& yP) {
   Fp2 ZZ = fp2_sqr(T.Z);
   Fp2 U2 = fp2_mul(Q.x, ZZ);
   Fp2 S2 = fp2_mul(fp2_mul(Q.y, T.Z), ZZ);
@@ -55,6 +55,9 @@ TBG_PT Line miller_add(G2J& T, const G2A& Q, const Fp& nxP, const Fp& yP) {
   T = {X3, Y3, Z3};
   return l;
 }
+
+TBG_NI Line miller_dbl(G2J& T, const Fp& nxP, const Fp& yP) { return miller_dbl_in(T, nxP, yP); }
+TBG_NI Line miller_add(G2J& T, const G2A& Q, const Fp& nxP, const Fp& yP) { return miller_add_in(T, Q, nxP, yP); }
 
 // prod_n f_{|x|, Q_n}(P_n), conjugated for x < 0.  P, Q must not be infinity.
 template <int N>

@@ -154,8 +154,9 @@ TBG_DEV int quad_lane() {
   return q > 2 ? 2 : q;
 }
 
-// C = A * B (both quad-distributed)
-__device__ TBG_QUAD_FN Fp4 quad_mul(const Fp4& A, const Fp4& B) {
+// C = A * B (both quad-distributed).  The _in bodies are for kernel loops;
+// the out-of-line forms serve the final exponentiation's callable loops.
+TBG_DEV Fp4 quad_mul_in(const Fp4& A, const Fp4& B) {
   int q = quad_lane();
   Fp4 SA = fp4_add(xch<QP_NEXT>(A), xch<QP_PREV>(A));
   Fp4 SB = fp4_add(xch<QP_NEXT>(B), xch<QP_PREV>(B));
@@ -164,7 +165,7 @@ __device__ TBG_QUAD_FN Fp4 quad_mul(const Fp4& A, const Fp4& B) {
   return quad_combine(q, P, xch<QP_NEXT>(P), xch<QP_PREV>(P), xch<QP_SW12>(Q));
 }
 
-__device__ TBG_QUAD_FN Fp4 quad_sqr(const Fp4& A) {
+TBG_DEV Fp4 quad_sqr_in(const Fp4& A) {
   int q = quad_lane();
   Fp4 SA = fp4_add(xch<QP_NEXT>(A), xch<QP_PREV>(A));
   Fp4 P = fp4_sqr(A);
@@ -172,13 +173,20 @@ __device__ TBG_QUAD_FN Fp4 quad_sqr(const Fp4& A) {
   return quad_combine(q, P, xch<QP_NEXT>(P), xch<QP_PREV>(P), xch<QP_SW12>(Q));
 }
 
-__device__ TBG_QUAD_FN Fp4 quad_cyc_sqr(const Fp4& A) {
+TBG_DEV Fp4 quad_cyc_sqr_in(const Fp4& A) {
   Fp4 T = fp4_sqr(A);
   return quad_cyc_lane(quad_lane(), A, xch<QP_SW12>(T));
 }
 
-__device__ TBG_QUAD_FN Fp4 quad_line(const Fp4& A, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
+TBG_DEV Fp4 quad_line_in(const Fp4& A, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
   return quad_line_lane(quad_lane(), A, xch<QP_NEXT>(A), l0, l1, l4);
+}
+
+__device__ TBG_QUAD_FN Fp4 quad_mul(const Fp4& A, const Fp4& B) { return quad_mul_in(A, B); }
+__device__ TBG_QUAD_FN Fp4 quad_sqr(const Fp4& A) { return quad_sqr_in(A); }
+__device__ TBG_QUAD_FN Fp4 quad_cyc_sqr(const Fp4& A) { return quad_cyc_sqr_in(A); }
+__device__ TBG_QUAD_FN Fp4 quad_line(const Fp4& A, const Fp2& l0, const Fp2& l1, const Fp2& l4) {
+  return quad_line_in(A, l0, l1, l4);
 }
 
 TBG_DEV Fp4 quad_conj(const Fp4& A) { return quad_conj_lane(quad_lane(), A); }

@@ -44,8 +44,8 @@ TBG_HD G2A g2_psi_aff(const G2A& a) {
   return {fp2_mul(fp2_conj(a.x), fp2_from_const(PSI_X)), fp2_mul(fp2_conj(a.y), fp2_from_const(PSI_Y))};
 }
 
-// sum_k a_k psi^k(s) for s in G2 (affine), a_k < 2^16
-TBG_NI G2J rlc_mul_g2(const G2A& s, const uint32_t (&a)[4]) {
+// sum_k a_k psi^k(s) for s in G2 (affine), a_k < 2^16 (steps inlined: kernel callers)
+TBG_HD G2J rlc_mul_g2(const G2A& s, const uint32_t (&a)[4]) {
   G2A q[4];
   q[0] = s;
   q[1] = g2_psi_aff(q[0]);
@@ -54,18 +54,18 @@ TBG_NI G2J rlc_mul_g2(const G2A& s, const uint32_t (&a)[4]) {
   G2J acc = jac_inf<Fp2>();
   bool started = false;
   for (int bit = 15; bit >= 0; --bit) {
-    if (started) acc = jac_dbl(acc);
+    if (started) acc = jac_dbl_in(acc);
     for (int k = 0; k < 4; ++k)
       if ((a[k] >> bit) & 1) {
-        acc = jac_add_aff(acc, q[k]);
+        acc = jac_add_aff_in(acc, q[k]);
         started = true;
       }
   }
   return acc;
 }
 
-// a_0 pk + a_1 xpk - a_2 phi(pk) - a_3 phi(xpk), xpk = [x]pk
-TBG_NI G1J rlc_mul_g1(const G1A& pk, const G1A& xpk, const uint32_t (&a)[4]) {
+// a_0 pk + a_1 xpk - a_2 phi(pk) - a_3 phi(xpk), xpk = [x]pk (steps inlined: kernel callers)
+TBG_HD G1J rlc_mul_g1(const G1A& pk, const G1A& xpk, const uint32_t (&a)[4]) {
   const Fp beta = fp_from_const(G1_BETA);
   G1A q[4];
   q[0] = pk;
@@ -75,10 +75,10 @@ TBG_NI G1J rlc_mul_g1(const G1A& pk, const G1A& xpk, const uint32_t (&a)[4]) {
   G1J acc = jac_inf<Fp>();
   bool started = false;
   for (int bit = 15; bit >= 0; --bit) {
-    if (started) acc = jac_dbl(acc);
+    if (started) acc = jac_dbl_in(acc);
     for (int k = 0; k < 4; ++k)
       if ((a[k] >> bit) & 1) {
-        acc = jac_add_aff(acc, q[k]);
+        acc = jac_add_aff_in(acc, q[k]);
         started = true;
       }
   }

@@ -33,7 +33,7 @@ __global__ void TBG_LAUNCH k_decode_sigs(DevBatch B) {
   uint8_t b[96];
   for (int j = 0; j < 96; ++j) b[j] = B.sigs[96ull * i + j];
   G2A a;
-  int32_t st = g2_decompress(b, a);
+  int32_t st = g2_decompress_t<true>(b, a);
   if (st == DEC_IDENTITY) st = TBG_PS_ERR_IDENTITY;
   if (st != DEC_OK) {
     a.x = fp2_zero();

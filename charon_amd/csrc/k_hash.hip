@@ -8,7 +8,7 @@ __global__ void TBG_LAUNCH k_hash_msgs(DevBatch B) {
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= B.n_msgs) return;
   uint32_t off = B.msg_off[m], len = B.msg_off[m + 1] - off;
-  G2J h = hash_to_g2(B.msgs + off, len);
+  G2J h = hash_to_g2_t<true>(B.msgs + off, len);
   G2A a;
   bool ok = jac_to_aff(h, a);
   if (!ok) {

@@ -125,13 +125,14 @@ __global__ void TBG_LAUNCH k_rlc_group_lines(DevBatch B) {
     return;
   }
   Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines(Sa, nx, fp_from_const(G1_NEG_Y), B.grp_lines + (size_t)LINES_WORDS * g);
+  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.grp_lines + (size_t)LINES_WORDS * g);
   B.grp_state[g] = GRP_LINES;
 }
 
 // f *= line(H(m) lines at step idx) evaluated at affine P = (-x, y).  The
 // two evaluation products are split over the quad (lane 0: l1 (-x), lane 1:
 // l4 y) and broadcast, instead of every lane computing both.
+template <bool INL = false>
 __device__ __forceinline__ Fp4 quad_line_at(const Fp4& f, const uint32_t* lines, int idx, const Fp& nx, const Fp& y) {
   const uint32_t* src = lines + LINE_WORDS * idx;
   const bool first = (threadIdx.x & 3) == 0;
@@ -143,11 +144,12 @@ __device__ __forceinline__ Fp4 quad_line_at(const Fp4& f, const uint32_t* lines,
     lk.c1.l[i] = first ? src[3 * NL + i] : src[5 * NL + i];
   }
   Fp2 e = fp2_mul_fp(lk, first ? nx : y);
-  return quad_line(f, l0, xch<QP_B0>(e), xch<QP_B1>(e));
+  return INL ? quad_line_in(f, l0, xch<QP_B0>(e), xch<QP_B1>(e)) : quad_line(f, l0, xch<QP_B0>(e), xch<QP_B1>(e));
 }
+template <bool INL = false>
 __device__ __forceinline__ Fp4 quad_line_folded(const Fp4& f, const uint32_t* lines, int idx) {
   Line a = line_load(lines + LINE_WORDS * idx);
-  return quad_line(f, a.l0, a.l1, a.l4);
+  return INL ? quad_line_in(f, a.l0, a.l1, a.l4) : quad_line(f, a.l0, a.l1, a.l4);
 }
 
 // Quad-layout Fp12 in HBM: lane q < 3 owns one Fp4 (4 NL words).
@@ -186,16 +188,16 @@ __global__ void TBG_LAUNCH k_rlc_miller_chunks(DevBatch B) {
   Fp4 f = quad_one();
   int idx = 0;
   for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = quad_sqr(f);
+    if (b != 62) f = quad_sqr_in(f);
     int steps = ((X_ABS >> b) & 1) ? 2 : 1;
     for (int s = 0; s < steps; ++s, ++idx) {
-      if (c == 0) f = quad_line_folded(f, ls, idx);
+      if (c == 0) f = quad_line_folded<true>(f, ls, idx);
       for (uint32_t d = d0; d < d1; ++d) {
         if (B.dv_state[d] != RLC_COMBINED) continue;
         uint32_t m = B.duty_msg[d];
         if (B.h_status[m] != 0) continue;  // the group fails in k_rlc_group_final
         const G1A& P = B.dv_p[d];
-        f = quad_line_at(f, B.h_lines + (size_t)LINES_WORDS * m, idx, fp_reduce(fp_neg(P.x)), P.y);
+        f = quad_line_at<true>(f, B.h_lines + (size_t)LINES_WORDS * m, idx, fp_reduce(fp_neg(P.x)), P.y);
       }
     }
   }
@@ -259,7 +261,7 @@ __global__ void TBG_LAUNCH k_rlc_duty_lines(DevBatch B) {
   G2A Sa;
   if (!jac_to_aff(B.dv_s[d], Sa)) return;  // excluded in k_rlc_duty_sum
   Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines(Sa, nx, fp_from_const(G1_NEG_Y), B.dv_lines + (size_t)LINES_WORDS * k);
+  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.dv_lines + (size_t)LINES_WORDS * k);
 }
 
 // Level 2 check: one quad per listed duty; failures go to level 3.
@@ -309,7 +311,7 @@ __global__ void TBG_LAUNCH k_lines_sig_list(DevBatch B) {
   if (k >= B.counters[CNT_PARTIALS]) return;
   uint32_t i = B.part_list[k];
   Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines(B.sig_aff[i], nx, fp_from_const(G1_NEG_Y), B.sig_lines + (size_t)LINES_WORDS * k);
+  g2_lines_t<true>(B.sig_aff[i], nx, fp_from_const(G1_NEG_Y), B.sig_lines + (size_t)LINES_WORDS * k);
 }
 
 // Level 3 check: one quad per listed partial, the exact CoreVerify.

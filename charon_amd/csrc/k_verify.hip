@@ -12,7 +12,7 @@ __global__ void TBG_LAUNCH k_lines_h(DevBatch B) {
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= B.n_msgs) return;
   if (B.h_status[m] != 0) return;
-  g2_lines(B.h_aff[m], fp_one(), fp_one(), B.h_lines + (size_t)LINES_WORDS * m);
+  g2_lines_t<true>(B.h_aff[m], fp_one(), fp_one(), B.h_lines + (size_t)LINES_WORDS * m);
 }
 
 void launch_h_lines(const DevBatch& B, hipStream_t st) {
