@@ -104,6 +104,81 @@ def work_model():
     return None
 
 
+# Stages of the kernel chain (tbg_last_timings order) and their kernels.
+STAGE_KERNELS = {
+    "decode": ["k_decode_sigs"],
+    "hash": ["k_hash_msgs"],
+    "combine": ["k_rlc_partial", "k_rlc_duty_sum", "k_rlc_group_lines"],
+    "h_lines": ["k_lines_h"],
+    "verify": ["k_rlc_miller_chunks", "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_duty_lines",
+               "k_rlc_check_duties", "k_lines_sig_list", "k_verify_list"],
+    "aggregate": ["k_lagrange", "k_aggregate"],
+}
+
+
+def stage_mads(wm, args):
+    """Algorithmic u32 mul-adds per launch of each stage for one clean batch
+    (work model of tools/count_work.py: RLC group G = 8, chunk C = 2)."""
+    m = wm["mads"]
+    nd, n = args.dvs, args.n
+    np_ = nd * n
+    G = wm.get("rlc_schedule", {}).get("group", 8)
+    ng = (nd + G - 1) // G
+    return {
+        "decode": m["decode_sig"] * np_,
+        "hash": m["hash_to_g2"] * nd,
+        "combine": m["rlc_partial"] * (np_ - nd) + m["rlc_duty_sum_4"] * nd + m["rlc_group_lines_8"] * ng,
+        "h_lines": m["lines_h"] * nd,
+        "verify": m["rlc_check_per_group"] * ng,
+        "aggregate": m["aggregate_3of4_all4"] * nd,
+    }
+
+
+def traffic_model():
+    """Per-kernel HBM bytes per launch from the committed PMC passes of this
+    build (profiles/traffic_latest.json, written by tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def stage_rooflines(wm, iso, args, value):
+    if not wm or args.t != 3 or args.n != 4:
+        return None, None
+    mads = stage_mads(wm, args)
+    stage = max(mads, key=lambda k: iso.get(k, 0.0))  # dominant stage of the isolated batch
+    ms = iso[stage]
+    achieved = mads[stage] / (ms * 1e-3) / 1e12
+    traffic = None
+    tm = traffic_model()
+    if tm:
+        kk = tm.get("kernels", {})
+        if all(k in kk for k in STAGE_KERNELS[stage][:2]):
+            traffic = int(sum(1024 * (kk[k].get("FETCH_SIZE_KB_per_launch", 0) + kk[k].get("WRITE_SIZE_KB_per_launch", 0))
+                              for k in STAGE_KERNELS[stage] if k in kk))
+    roofline = {"bound": "valu-int-mul", "kernel": f"{stage} stage: " + " + ".join(STAGE_KERNELS[stage][:3]),
+                "achieved": round(achieved, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
+                "frac": round(achieved / PEAK_MAD_TOPS, 4), "traffic": traffic,
+                "algorithmic_mads_per_launch": int(mads[stage]), "launch_ms": round(ms, 3)}
+    unit = wm["mads"]["unit_3of4_rlc"]
+    ach_p = value * unit / 1e12
+    step_traffic = None
+    if tm:
+        step_traffic = int(sum(1024 * (v.get("FETCH_SIZE_KB_per_launch", 0) + v.get("WRITE_SIZE_KB_per_launch", 0))
+                               for k, v in tm.get("kernels", {}).items() if any(k in ks for ks in STAGE_KERNELS.values())))
+    pipeline = {"bound": "valu-int-mul",
+                "kernel": "the whole kernel chain of one step (batches pipelined, kernels of 8 batches overlap, so "
+                          "per-kernel durations are not separable in the timed region)",
+                "achieved": round(ach_p, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
+                "frac": round(ach_p / PEAK_MAD_TOPS, 4), "traffic": step_traffic,
+                "work_per_unit_mads": unit,
+                "reference_schedule_mads_per_unit": wm["mads"]["unit_3of4_single_lane_schedule"],
+                "reference_schedule_equivalent_tmads": round(value * wm["mads"]["unit_3of4_single_lane_schedule"] / 1e12, 3)}
+    return roofline, pipeline
+
+
 def cpu_baseline(batch, seconds: float):
     """The oracle (CPU restatement, 'port') on a bounded sample of the same
     workload: whole DV-duties (n verifies + 1 combine), all host threads."""
@@ -176,17 +251,11 @@ def main():
     value = units / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    wm = work_model()
-    roofline = None
-    if wm:
-        key = f"{args.t}of{args.n}"
-        per_verify = wm["mads"]["verify_quad_item"]
-        verify_ms = kernel_ms["verify"] / args.steps
-        achieved = per_verify * args.dvs * args.n / (verify_ms * 1e-3) / 1e12
-        roofline = {"bound": "valu-int-mul", "kernel": "k_verify_quad", "achieved": round(achieved, 3),
-                    "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s", "frac": round(achieved / PEAK_MAD_TOPS, 4),
-                    "traffic": wm.get("verify_hbm_bytes_per_launch"),
-                    "work_per_unit_mads": wm["mads"].get("unit_" + key)}
+    # Isolated pass (untimed): one resident batch alone on the GPU, per-stage
+    # HIP events on its stream -- the per-launch durations the roofline uses
+    # (under 8-way pipelining every stage shares the CUs with 7 other batches).
+    iso = e.replay(tickets[0], 1)
+    roofline_isolated, roofline = stage_rooflines(work_model(), iso, args, value)
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "DV-duties/s (n verifies + 1 aggregate each)",
@@ -198,7 +267,9 @@ def main():
                    "inflight_batches": args.inflight, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),
+        "isolated_batch_ms": {k: round(v, 3) for k, v in iso.items()},
         "roofline": roofline,
+        "roofline_isolated": roofline_isolated,
         "cpu_baseline": None,
     }
     if rank == 0 and not args.no_cpu and ws == 1:

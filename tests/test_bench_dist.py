@@ -48,3 +48,20 @@ def test_two_rank_max_over_ranks():
     # both ranks report the same (max) elapsed time, at least the slow rank's 0.2 s
     assert abs(dts[0] - dts[1]) < 1e-9
     assert dts[0] >= 0.2
+
+
+def test_roofline_fields_from_work_model():
+    """bench.py's roofline arithmetic (no GPU): the pipelined chain's
+    achieved rate is units/s x algorithmic mul-adds per unit; the isolated
+    stage's is its mul-adds per launch / its launch time."""
+    import argparse
+    import bench
+    wm = bench.work_model()
+    assert wm is not None
+    args = argparse.Namespace(dvs=10000, t=3, n=4)
+    iso = {"decode": 2.8, "hash": 6.6, "combine": 8.4, "h_lines": 2.5, "verify": 11.2, "aggregate": 0.8}
+    stage, pipe = bench.stage_rooflines(wm, iso, args, 1.0e6)
+    assert stage["kernel"].startswith("verify stage")
+    assert abs(stage["achieved"] - stage["algorithmic_mads_per_launch"] / 11.2e-3 / 1e12) < 1e-2
+    assert abs(pipe["achieved"] - 1.0e6 * wm["mads"]["unit_3of4_rlc"] / 1e12) < 1e-2
+    assert 0 < pipe["frac"] < 1

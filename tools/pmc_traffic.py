@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic (KB per launch) from the two rocprofv3 PMC passes
+of tools/gpu_round.sh (FETCH_SIZE and WRITE_SIZE in separate runs, as
+MI355X_MICROARCH.md prescribes) -> JSON for profiles/ and bench.py.
+
+  python tools/pmc_traffic.py gpurun_out/round profiles/rNN/traffic.json
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def main(src, dst):
+    out = {}
+    for sub, c in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+        agg = collections.defaultdict(list)
+        with open(os.path.join(src, sub, "run_counter_collection.csv")) as f:
+            for r in csv.DictReader(f):
+                if r["Counter_Name"] == c:
+                    agg[r["Kernel_Name"].split("(")[0].replace("tbg::", "")].append(float(r["Counter_Value"]))
+        for k, v in agg.items():
+            out.setdefault(k, {})[c + "_KB_per_launch"] = round(sum(v) / len(v), 1)
+            out[k]["launches"] = len(v)
+    doc = {"command": "rocprofv3 --pmc FETCH_SIZE (resp. WRITE_SIZE) -f csv -- python3 bench.py --no-cpu --steps 4 "
+                      "--inflight 1 (tools/gpu_round.sh)",
+           "note": "one counter group per pass; raw values in KB per launch; FETCH_SIZE not doubled (the gfx950 x2 "
+                   "correction is calibrated only for 16-B/lane streaming reads); batch = 10k 3-of-4 DVs",
+           "kernels": out}
+    with open(dst, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
