@@ -98,6 +98,14 @@ template <class F> TBG_HD Jac<F> jac_add_in(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // Mixed addition P (Jacobian) + Q (affine), exceptional cases handled.
+// TBG_ADD_DBL_INLINE=1: the P == Q case doubles inline (no out-of-line call
+// in the caller's loop, whose live registers would otherwise be saved around
+// the call site).
+#if defined(TBG_ADD_DBL_INLINE) && TBG_ADD_DBL_INLINE
+#define TBG_ADD_DBL(p) jac_dbl_in(p)
+#else
+#define TBG_ADD_DBL(p) jac_dbl(p)
+#endif
 template <class F> TBG_HD Jac<F> jac_add_aff_in(const Jac<F>& p, const Aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.Z);
@@ -106,7 +114,7 @@ template <class F> TBG_HD Jac<F> jac_add_aff_in(const Jac<F>& p, const Aff<F>& q
   F H = f_reduce(f_sub(U2, p.X));
   F Rr = f_reduce(f_sub(S2, p.Y));
   if (f_is_zero(H)) {
-    if (f_is_zero(Rr)) return jac_dbl(p);
+    if (f_is_zero(Rr)) return TBG_ADD_DBL(p);
     return jac_inf<F>();
   }
   F HH = f_sqr(H);

@@ -1,15 +1,21 @@
 // Random-linear-combination scalars and their application (k_rlc.hip).
 //
-// r_i is 64 secret random bits read as four 16-bit digits a_k of
-//   r_i = a_0 + a_1 x + a_2 x^2 + a_3 x^3   (x = -0xd201000000010000).
-// Distinct digit vectors give distinct r_i mod r (2^16 < |x| and
-// 2^16 |x|^3 < r), so the usual RLC bound (a false accept <= 1/2^64) holds.
+// r_i is 64 secret random bits u, split into four 16-bit words u_k and read
+// as SIGNED binary digits (bit j of u_k set -> +1, clear -> -1):
+//   a_k = sum_j e_kj 2^j = 2 u_k - (2^16 - 1)   (odd, |a_k| < 2^16)
+//   r_i = a_0 + a_1 x + a_2 x^2 + a_3 x^3      (x = -0xd201000000010000).
+// Distinct u give distinct r_i mod r (digit differences are < 2^17 < |x| and
+// 2^17 |x|^3 < r), so the usual RLC bound (a false accept <= 1/2^64) holds.
 // For a signature s that passed the subgroup check psi(s) = [x] s, and on G1
 // [x^2] = -phi (phi(x, y) = (beta x, y)), so
-//   [r] s  = sum_k a_k psi^k(s)
+//   [r] s  = sum_k a_k psi^k(s)  = T(s, psi(s))   + psi^2 T'(s, psi(s))
 //   [r] pk = a_0 pk + a_1 [x]pk - a_2 phi(pk) - a_3 phi([x]pk)
-// are four-point Straus products with 16-bit scalars (15 doublings instead
-// of 63), given [x]pk from the resident key table.
+//          = T(pk, [x]pk) - phi T'(pk, [x]pk)
+// with psi^2(x, y) = (PSI2_X x, -y) and -phi(x, y) = (beta x, -y).  Every
+// digit is non-zero, so each of the 16 bit positions adds exactly one entry
+// of {+-(q0 + q1), +-(q0 - q1)} per pair: 15 doublings + 31 additions in
+// uniform control flow.  (Unsigned 0/1 digits made the additions of the
+// four points lane-divergent: a wave executed all 64 of them, masked.)
 #pragma once
 #include "bls_h2c.h"
 
@@ -36,53 +42,98 @@ TBG_HD uint64_t rlc_scalar(const uint32_t (&seed)[8], uint32_t i) {
   return r ? r : 1;
 }
 
-TBG_HD void rlc_digits(uint64_t r, uint32_t (&a)[4]) {
-  for (int k = 0; k < 4; ++k) a[k] = (uint32_t)((r >> (16 * k)) & 0xFFFF);
+TBG_HD void rlc_digits(uint64_t r, uint32_t (&u)[4]) {
+  for (int k = 0; k < 4; ++k) u[k] = (uint32_t)((r >> (16 * k)) & 0xFFFF);
 }
 
 TBG_HD G2A g2_psi_aff(const G2A& a) {
   return {fp2_mul(fp2_conj(a.x), fp2_from_const(PSI_X)), fp2_mul(fp2_conj(a.y), fp2_from_const(PSI_Y))};
 }
 
-// sum_k a_k psi^k(s) for s in G2 (affine), a_k < 2^16 (steps inlined: kernel callers)
-TBG_HD G2J rlc_mul_g2(const G2A& s, const uint32_t (&a)[4]) {
-  G2A q[4];
-  q[0] = s;
-  q[1] = g2_psi_aff(q[0]);
-  q[2] = g2_psi_aff(q[1]);
-  q[3] = g2_psi_aff(q[2]);
-  G2J acc = jac_inf<Fp2>();
-  bool started = false;
-  for (int bit = 15; bit >= 0; --bit) {
-    if (started) acc = jac_dbl_in(acc);
-    for (int k = 0; k < 4; ++k)
-      if ((a[k] >> bit) & 1) {
-        acc = jac_add_aff_in(acc, q[k]);
-        started = true;
-      }
+TBG_HD Fp rlc_mul_c(const Fp& a, const Fp& c) { return fp_mul(a, c); }
+TBG_HD Fp2 rlc_mul_c(const Fp2& a, const Fp& c) { return fp2_mul_fp(a, c); }
+
+// Table entry e0 q0 + e1 q1 (e = +-1 from bits b0, b1) out of A+ = q0 + q1
+// and A- = q0 - q1; `endo` maps it through (x, y) -> (c x, -y).  The sign is
+// applied by negating the selected y (cheaper than keeping -y resident).
+template <class F>
+TBG_HD Aff<F> rlc_entry(const Aff<F>& ap, const Aff<F>& am, uint32_t b0, uint32_t b1, bool endo, const Fp& c) {
+  const bool same = b0 == b1;
+  const bool negy = (b0 != 0) == endo;  // -(..) for b0 = 0, and endo negates y once more
+  Aff<F> e;
+  e.x = same ? ap.x : am.x;
+  const F y = same ? ap.y : am.y;
+  const F ny = f_reduce(f_neg(y));
+  e.y = negy ? ny : y;
+  if (endo) e.x = rlc_mul_c(e.x, c);
+  return e;
+}
+
+// A+ = q0 + q1 and A- = q0 - q1 in affine form given inv = 1 / (x1 - x0)
+// (q0 != +-q1: both are non-identity points of prime order r and
+// q1 = [x] q0 or psi(q0) = [x] q0 with x != +-1 mod r).
+template <class F>
+TBG_HD void rlc_pair_from_inv(const Aff<F>& q0, const Aff<F>& q1, const F& inv, Aff<F>& ap, Aff<F>& am) {
+  const F lp = f_mul(f_reduce(f_sub(q1.y, q0.y)), inv);
+  // decoded coordinates may be up to 16p (a negated root): reduce the sums
+  const F lm = f_mul(f_reduce(f_neg(f_reduce(f_add(q1.y, q0.y)))), inv);
+  const F xs = f_reduce(f_add(q0.x, q1.x));
+  ap.x = f_reduce(f_sub(f_sqr(lp), xs));
+  ap.y = f_reduce(f_sub(f_mul(lp, f_reduce(f_sub(q0.x, ap.x))), q0.y));
+  am.x = f_reduce(f_sub(f_sqr(lm), xs));
+  am.y = f_reduce(f_sub(f_mul(lm, f_reduce(f_sub(q0.x, am.x))), q0.y));
+}
+
+// sum_j 2^j (e0j q0 + e1j q1 + endo(e2j q0 + e3j q1)) from the pair table
+// A+-, digits u (see top).
+template <class F>
+TBG_HD Jac<F> rlc_mul_table(const Aff<F>& ap, const Aff<F>& am, const Fp& c, const uint32_t (&u)[4]) {
+  Jac<F> acc = jac_from_aff(rlc_entry(ap, am, (u[0] >> 15) & 1, (u[1] >> 15) & 1, false, c));
+  acc = jac_add_aff_in(acc, rlc_entry(ap, am, (u[2] >> 15) & 1, (u[3] >> 15) & 1, true, c));
+#pragma unroll 1
+  for (int bit = 14; bit >= 0; --bit) {
+    acc = jac_dbl_in(acc);
+    acc = jac_add_aff_in(acc, rlc_entry(ap, am, (u[0] >> bit) & 1, (u[1] >> bit) & 1, false, c));
+    acc = jac_add_aff_in(acc, rlc_entry(ap, am, (u[2] >> bit) & 1, (u[3] >> bit) & 1, true, c));
   }
   return acc;
 }
 
-// a_0 pk + a_1 xpk - a_2 phi(pk) - a_3 phi(xpk), xpk = [x]pk (steps inlined: kernel callers)
-TBG_HD G1J rlc_mul_g1(const G1A& pk, const G1A& xpk, const uint32_t (&a)[4]) {
-  const Fp beta = fp_from_const(G1_BETA);
-  G1A q[4];
-  q[0] = pk;
-  q[1] = xpk;
-  q[2] = {fp_mul(pk.x, beta), fp_reduce(fp_neg(pk.y))};
-  q[3] = {fp_mul(xpk.x, beta), fp_reduce(fp_neg(xpk.y))};
-  G1J acc = jac_inf<Fp>();
-  bool started = false;
-  for (int bit = 15; bit >= 0; --bit) {
-    if (started) acc = jac_dbl_in(acc);
-    for (int k = 0; k < 4; ++k)
-      if ((a[k] >> bit) & 1) {
-        acc = jac_add_aff_in(acc, q[k]);
-        started = true;
-      }
+// [r] s for s in G2 (affine): pairs (s, psi(s)) and psi^2 of the same table.
+TBG_HD G2J rlc_mul_g2(const G2A& s, const uint32_t (&u)[4]) {
+  const G2A ps = g2_psi_aff(s);
+  G2A ap, am;
+  rlc_pair_from_inv(s, ps, fp2_inv(fp2_reduce(fp2_sub(ps.x, s.x))), ap, am);
+  return rlc_mul_table(ap, am, fp_from_const(PSI2_X), u);
+}
+
+// [r] pk on G1: pairs (pk, [x]pk) and -phi of the same table.
+TBG_HD G1J rlc_mul_g1(const G1A& pk, const G1A& xpk, const uint32_t (&u)[4]) {
+  G1A ap, am;
+  rlc_pair_from_inv(pk, xpk, fp_inv(fp_reduce(fp_sub(xpk.x, pk.x))), ap, am);
+  return rlc_mul_table(ap, am, fp_from_const(G1_BETA), u);
+}
+
+// Both products of one partial (k_rlc_partial) with ONE field inversion for
+// the two tables (Montgomery's trick on dx1 and the norm n2 of dx2):
+// t = 1 / (dx1 n2), 1/dx1 = t n2, 1/dx2 = conj(dx2) t dx1.
+TBG_HD void rlc_mul_both(const G2A& s, const G1A& pk, const G1A& xpk, const uint32_t (&u)[4], G2J& S, G1J& P) {
+  const G2A ps = g2_psi_aff(s);
+  const Fp2 dx2 = fp2_reduce(fp2_sub(ps.x, s.x));
+  const Fp dx1 = fp_reduce(fp_sub(xpk.x, pk.x));
+  const Fp n2 = fp_mul2(dx2.c0, dx2.c0, dx2.c1, dx2.c1);
+  const Fp t = fp_inv(fp_mul(n2, dx1));
+  const Fp in2 = fp_mul(t, dx1);
+  {
+    G2A ap, am;
+    rlc_pair_from_inv(s, ps, Fp2{fp_mul(dx2.c0, in2), fp_mul(fp_neg(dx2.c1), in2)}, ap, am);
+    S = rlc_mul_table(ap, am, fp_from_const(PSI2_X), u);
   }
-  return acc;
+  {
+    G1A ap, am;
+    rlc_pair_from_inv(pk, xpk, fp_mul(t, n2), ap, am);
+    P = rlc_mul_table(ap, am, fp_from_const(G1_BETA), u);
+  }
 }
 
 }  // namespace tbg

@@ -68,8 +68,9 @@ __global__ void TBG_LAUNCH k_rlc_partial(DevBatch B, const G1A* pk_aff, const G1
   }
   uint32_t a[4];
   rlc_digits(rlc_scalar(B.rlc_seed, i), a);
-  G2J S = rlc_mul_g2(s0, a);
-  G1J P = rlc_mul_g1(p0, xpk_aff[pid], a);
+  G2J S;
+  G1J P;
+  rlc_mul_both(s0, p0, xpk_aff[pid], a, S, P);
   B.part_s[i] = S;
   B.part_p[i] = P;
 }

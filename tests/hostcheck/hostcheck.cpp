@@ -356,9 +356,12 @@ int hc_rlc_check(const uint8_t* sig96, const uint8_t* pk48, uint64_t r64, const 
   rlc_digits(r64, a);
   G2J S = rlc_mul_g2(s, a);
   G1J P = rlc_mul_g1(pk, hc_xpk(pk), a);
+  G2J S2;
+  G1J P2;
+  rlc_mul_both(s, pk, hc_xpk(pk), a, S2, P2);
   G2J S_ref = jac_mul_words(jac_from_aff(s), r_words, 255);
   G1J P_ref = jac_mul_words(jac_from_aff(pk), r_words, 255);
-  return (jac_eq(S, S_ref) ? 1 : 0) | (jac_eq(P, P_ref) ? 2 : 0);
+  return (jac_eq(S, S_ref) && jac_eq(S2, S_ref) ? 1 : 0) | (jac_eq(P, P_ref) && jac_eq(P2, P_ref) ? 2 : 0);
 }
 uint64_t hc_rlc_scalar(const uint8_t* seed32, uint32_t i) {
   uint32_t seed[8];
@@ -380,8 +383,9 @@ int hc_stage_setup(const uint8_t* sig96, const uint8_t* pk48, const uint8_t* msg
 void hc_stage_rlc_partial(uint64_t r64) {
   uint32_t a[4];
   rlc_digits(r64, a);
-  G2J S = rlc_mul_g2(g_sig, a);
-  G1J P = rlc_mul_g1(g_pk, g_xpk, a);
+  G2J S;
+  G1J P;
+  rlc_mul_both(g_sig, g_pk, g_xpk, a, S, P);
   (void)S;
   (void)P;
 }

@@ -60,6 +60,14 @@ def b2f(b):
 
 
 def test_fp2_mul_and_sqrt():
+    # Karatsuba fp2_mul: c0 = REDC(a0 b0 - a1 b1) goes negative when a1 b1
+    # dominates (the conditional +p path); edge magnitudes on both sides
+    edges = [0, 1, 2, P - 1, P - 2, (P - 1) // 2, 1 << 380]
+    for a0 in edges:
+        for a1 in edges[:4]:
+            a, b = (a0, a1), (edges[3], a0)
+            assert b2f(call("hc_fp2_mul", f2b(a), f2b(b), out=96)) == bls.f2_mul(a, b)
+            assert b2f(call("hc_fp2_mul", f2b(b), f2b(a), out=96)) == bls.f2_mul(b, a)
     for _ in range(30):
         a = (rng.randrange(P), rng.randrange(P))
         b = (rng.randrange(P), rng.randrange(P))
@@ -260,7 +268,7 @@ def test_quad_verify_pipeline_emulated():
 
 
 def test_rlc_digit_scalars_match_plain_scalar_multiplication():
-    """k_rlc_partial applies r = a0 + a1 x + a2 x^2 + a3 x^3 through psi on G2
+    """k_rlc_partial applies r = a0 + a1 x + a2 x^2 + a3 x^3 (signed digits) through psi on G2
     and phi / [x]pk on G1; both must equal [r mod order] P."""
     import ctypes
     L = lib()
@@ -273,7 +281,8 @@ def test_rlc_digit_scalars_match_plain_scalar_multiplication():
         sig = bls.g2_compress(tb.sign(sk, msg))
         pk = bls.g1_compress(tb.sk_to_pk(sk))
         r64 = rng.getrandbits(64) if trial else 0xFFFF_FFFF_FFFF_FFFF
-        a = [(r64 >> (16 * k)) & 0xFFFF for k in range(4)]
+        # signed binary digits: bit set -> +1, clear -> -1 (bls_rlc.h)
+        a = [2 * ((r64 >> (16 * k)) & 0xFFFF) - 0xFFFF for k in range(4)]
         r = sum(a[k] * x ** k for k in range(4)) % bls.R
         words = (ctypes.c_uint32 * 8)(*[(r >> (32 * k)) & 0xFFFFFFFF for k in range(8)])
         assert L.hc_rlc_check(sig, pk, r64, words) == 3
@@ -283,4 +292,5 @@ def test_rlc_digit_scalars_are_distinct_mod_r():
     """Distinct digit vectors give distinct scalars (the 2^-64 soundness bound):
     |x| > 2^16 and 2^16 |x|^3 < r, checked on the extreme digit values."""
     x = bls.X_ABS
-    assert (1 << 16) < x and (1 << 16) * x ** 3 < bls.R
+    # signed digits a_k = 2 u_k - (2^16 - 1): differences of two are < 2^17
+    assert (1 << 17) < x and (1 << 17) * x ** 3 < bls.R
