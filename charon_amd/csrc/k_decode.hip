@@ -1,5 +1,8 @@
 // Decode kernels: 48-byte G1 pubkeys (tblsconv.KeyFromBytes, tblsconv.go:30-37)
 // and 96-byte G2 signatures (tblsconv.SigFromCore, tblsconv.go:125-132).
+// The P == Q case of the mixed addition doubles inline (bls_curve.h): no
+// out-of-line call inside the kernels' point loops.
+#define TBG_ADD_DBL_INLINE 1
 #include "tbls_launch.h"
 #include "bls_curve.h"
 

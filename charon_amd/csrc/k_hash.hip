@@ -1,4 +1,7 @@
 // hash_to_G2 per distinct message (the H(m) of SigEth2.Verify, tss.go:190-197).
+// The P == Q case of the mixed addition doubles inline (bls_curve.h): no
+// out-of-line call inside the kernels' point loops.
+#define TBG_ADD_DBL_INLINE 1
 #include "tbls_launch.h"
 #include "bls_h2c.h"
 

@@ -21,6 +21,9 @@
 // are shared by all partials of a message, the -g1 factor is folded into the
 // lines of S / S_d / s_i.  Work lists for levels 2 and 3 are compacted on the
 // device (atomic counters), so a clean batch launches them over empty lists.
+// The P == Q case of the mixed addition doubles inline (bls_curve.h): no
+// out-of-line call inside the kernels' point loops.
+#define TBG_ADD_DBL_INLINE 1
 #include "tbls_launch.h"
 #include "bls_h2c.h"
 #include "bls_lines.h"
