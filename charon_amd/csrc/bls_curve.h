@@ -69,6 +69,15 @@ template <class F> TBG_HD Jac<F> jac_dbl_in(const Jac<F>& p) {
   return {X3, Y3, Z3};
 }
 
+// TBG_ADD_DBL_INLINE=1: the P == Q case doubles inline (no out-of-line call
+// in the caller's loop, whose live registers would otherwise be saved around
+// the call site).
+#if defined(TBG_ADD_DBL_INLINE) && TBG_ADD_DBL_INLINE
+#define TBG_ADD_DBL(p) jac_dbl_in(p)
+#else
+#define TBG_ADD_DBL(p) jac_dbl(p)
+#endif
+
 // add-2007-bl with the exceptional cases handled (P == Q, P == -Q, infinity).
 template <class F> TBG_HD Jac<F> jac_add_in(const Jac<F>& p, const Jac<F>& q) {
   if (jac_is_inf(p)) return q;
@@ -98,14 +107,6 @@ template <class F> TBG_HD Jac<F> jac_add_in(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // Mixed addition P (Jacobian) + Q (affine), exceptional cases handled.
-// TBG_ADD_DBL_INLINE=1: the P == Q case doubles inline (no out-of-line call
-// in the caller's loop, whose live registers would otherwise be saved around
-// the call site).
-#if defined(TBG_ADD_DBL_INLINE) && TBG_ADD_DBL_INLINE
-#define TBG_ADD_DBL(p) jac_dbl_in(p)
-#else
-#define TBG_ADD_DBL(p) jac_dbl(p)
-#endif
 template <class F> TBG_HD Jac<F> jac_add_aff_in(const Jac<F>& p, const Aff<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   F Z1Z1 = f_sqr(p.Z);
@@ -187,6 +188,16 @@ template <class F> TBG_HD Jac<F> jac_mul_xabs_in(const Jac<F>& p) {
   return acc;
 }
 
+// [|x|] P for an affine P, doublings and (mixed) additions inline.
+template <class F> TBG_HD Jac<F> jac_mul_xabs_aff_in(const Aff<F>& p) {
+  Jac<F> acc = jac_from_aff(p);
+  for (int i = 62; i >= 0; --i) {
+    acc = jac_dbl_in(acc);
+    if ((X_ABS >> i) & 1) acc = jac_add_aff_in(acc, p);
+  }
+  return acc;
+}
+
 // [k] P for a multi-word scalar (little-endian 32-bit words, nbits significant).
 template <class F> TBG_NI Jac<F> jac_mul_words(const Jac<F>& p, const uint32_t* w, int nbits) {
   Jac<F> acc = jac_inf<F>();
@@ -212,6 +223,17 @@ TBG_HD bool g2_in_subgroup_in(const G2J& p) {
   if (jac_is_inf(p)) return true;
   G2J xp = jac_neg(jac_mul_xabs_in(p));  // [x]P, x < 0
   return jac_eq(g2_psi(p), xp);
+}
+// Affine input (decode): psi(a) == [x] a == -[|x|] a, compared in Jacobian
+// coordinates (X == x' Z^2, Y == -y' Z^3) without leaving the kernel body.
+TBG_HD bool g2_in_subgroup_aff_in(const G2A& a) {
+  const G2J m = jac_mul_xabs_aff_in(a);  // [|x|] a
+  const Fp2 px = fp2_mul(fp2_conj(a.x), fp2_from_const(PSI_X));
+  const Fp2 py = fp2_mul(fp2_conj(a.y), fp2_from_const(PSI_Y));
+  const Fp2 z2 = fp2_sqr(m.Z);
+  const Fp2 z3 = fp2_mul(z2, m.Z);
+  if (jac_is_inf(m)) return false;
+  return fp2_eq(fp2_mul(px, z2), m.X) && fp2_eq(fp2_mul(py, z3), fp2_reduce(fp2_neg(m.Y)));
 }
 TBG_NI bool g2_in_subgroup(const G2J& p) {
   if (jac_is_inf(p)) return true;
@@ -285,7 +307,7 @@ TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out) {
   if ((uint32_t)fp2_lex_largest(y) != s_flag) y = fp2_reduce(fp2_neg(y));
   out.x = x;
   out.y = y;
-  if (!(INL ? g2_in_subgroup_in(jac_from_aff(out)) : g2_in_subgroup(jac_from_aff(out)))) return DEC_ERR_SUBGROUP;
+  if (!(INL ? g2_in_subgroup_aff_in(out) : g2_in_subgroup(jac_from_aff(out)))) return DEC_ERR_SUBGROUP;
   return DEC_OK;
 }
 TBG_NI int32_t g2_decompress(const uint8_t* b, G2A& out) { return g2_decompress_t<false>(b, out); }

@@ -71,8 +71,10 @@ void hc_final_exp(const uint8_t* a, uint8_t* out) { f12_out(final_exp(f12_in(a))
 // G2 decompress -> status; on success writes the recompressed encoding and
 // affine coordinates (x0, x1, y0, y1; 48 bytes each).
 int hc_g2_decompress(const uint8_t* in, uint8_t* aff_out) {
-  G2A a;
+  G2A a, b;
   int st = g2_decompress(in, a);
+  // the kernel's form (inline subgroup check on the affine point) must agree
+  if (g2_decompress_t<true>(in, b) != st) return 99;
   if (st == DEC_OK) {
     to_be(a.x.c0, aff_out);
     to_be(a.x.c1, aff_out + 48);
@@ -126,7 +128,7 @@ int hc_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t len, const uint8
 // Work-model probes: each runs one item of a pipeline stage.
 int hc_stage_decode_sig(const uint8_t* sig96) {
   G2A a;
-  return g2_decompress(sig96, a);
+  return g2_decompress_t<true>(sig96, a);  // k_decode_sigs' form
 }
 int hc_stage_verify(const uint8_t* pk48, const uint8_t* sig96, const uint8_t* msg, uint32_t len) {
   G1A pk;
