@@ -118,16 +118,16 @@ STAGE_KERNELS = {
 
 def stage_mads(wm, args):
     """Algorithmic u32 mul-adds per launch of each stage for one clean batch
-    (work model of tools/count_work.py: RLC group G = 8, chunk C = 2)."""
+    (work model of tools/count_work.py: RLC group G = 16, chunk C = 4)."""
     m = wm["mads"]
     nd, n = args.dvs, args.n
     np_ = nd * n
-    G = wm.get("rlc_schedule", {}).get("group", 8)
+    G = wm.get("rlc_schedule", {}).get("group", 16)
     ng = (nd + G - 1) // G
     return {
         "decode": m["decode_sig"] * np_,
         "hash": m["hash_to_g2"] * nd,
-        "combine": m["rlc_partial"] * (np_ - nd) + m["rlc_duty_sum_4"] * nd + m["rlc_group_lines_8"] * ng,
+        "combine": m["rlc_partial"] * (np_ - nd) + m["rlc_duty_sum_4"] * nd + m["rlc_group_lines"] * ng,
         "h_lines": m["lines_h"] * nd,
         "verify": m["rlc_check_per_group"] * ng,
         "aggregate": m["aggregate_3of4_all4"] * nd,

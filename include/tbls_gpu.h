@@ -77,9 +77,9 @@ typedef struct {
   uint32_t max_msg_bytes;
   uint32_t slots;         /* in-flight batches, each on its own streams (0 -> 3) */
   uint32_t verify_mode;   /* TBG_VERIFY_RLC (0, default) or TBG_VERIFY_EACH     */
-  uint32_t rlc_group;     /* duties per level-1 RLC group (0 -> 8)               */
+  uint32_t rlc_group;     /* duties per level-1 RLC group (0 -> 16)              */
   uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests) */
-  uint32_t rlc_chunk;     /* duties per Miller-loop quad inside a group (0 -> 2)  */
+  uint32_t rlc_chunk;     /* duties per Miller-loop quad inside a group (0 -> 4)  */
   uint32_t streams_per_slot; /* 1 (0 -> 1) or 2: hash_to_G2 on its own stream   */
 } tbg_config;
 

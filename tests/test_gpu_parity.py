@@ -31,8 +31,10 @@ SCHEDULES = {
     "each": dict(verify_mode=1),
     # random linear combinations: one duty per group (levels 1 -> 3)
     "rlc1": dict(verify_mode=0, rlc_group=1, rlc_seed=0x5EED),
-    # the default: 8 duties per group, fresh OS randomness per batch
-    "rlc8": dict(verify_mode=0),
+    # the default: 16 duties per group, 4 per Miller quad, fresh OS randomness per batch
+    "rlc16": dict(verify_mode=0),
+    # the previous default: 8 duties per group, 2 per quad
+    "rlc8c2": dict(verify_mode=0, rlc_group=8, rlc_chunk=2, rlc_seed=0x8C2),
     # large groups: most injected failures fall back through all three levels
     "rlc64": dict(verify_mode=0, rlc_group=64, rlc_seed=0xC0FFEE),
     # odd group / chunk sizes: ragged last group, chunks of 3 duties

@@ -58,7 +58,8 @@ def main():
     agg_with_decode = lib.hc_count_get()
     assert out.raw.hex() == gold["expect"]["agg"]
     agg = agg_with_decode - len(sigs) * decode
-    # RLC schedule (k_rlc.hip), default group G = 8 duties, chunk C = 2 duties
+    # RLC schedule (k_rlc.hip), default group G = 16 duties, chunk C = 4 duties
+    G, C = 16, 4
     for fn in ("hc_stage_setup", "hc_stage_rlc_partial", "hc_stage_duty_sum", "hc_stage_group_lines",
                "hc_stage_miller_chunk", "hc_stage_group_final"):
         getattr(lib, fn).restype = ctypes.c_int
@@ -66,11 +67,10 @@ def main():
     assert lib.hc_stage_setup(sigs[0], pks[0], msg, len(msg)) == 0
     rlc_partial, _ = measure(lib.hc_stage_rlc_partial, 0x9E3779B97F4A7C15)
     duty_sum4, _ = measure(lib.hc_stage_duty_sum, 4)
-    group_lines8, _ = measure(lib.hc_stage_group_lines, 8)
-    chunk2, _ = measure(lib.hc_stage_miller_chunk, 2, 0)
-    chunk2f, _ = measure(lib.hc_stage_miller_chunk, 2, 1)
-    final4, _ = measure(lib.hc_stage_group_final, 4)
-    G, C = 8, 2
+    group_lines8, _ = measure(lib.hc_stage_group_lines, G)
+    chunk2, _ = measure(lib.hc_stage_miller_chunk, C, 0)
+    chunk2f, _ = measure(lib.hc_stage_miller_chunk, C, 1)
+    final4, _ = measure(lib.hc_stage_group_final, G // C)
     rlc_check_per_group = chunk2f + (G // C - 1) * chunk2 + final4
     unit_3of4_rlc = (4 * decode + hash_ + lines_h + 3 * rlc_partial + duty_sum4 + group_lines8 / G
                      + rlc_check_per_group / G + agg)
@@ -82,8 +82,8 @@ def main():
         "rlc_schedule": {"group": G, "chunk": C},
         "mads": {"decode_sig": decode, "hash_to_g2": hash_, "lines_sig": lines_sig, "lines_h": lines_h,
                  "verify_quad_item": verify_quad, "verify_item_single_lane": verify,
-                 "rlc_partial": rlc_partial, "rlc_duty_sum_4": duty_sum4, "rlc_group_lines_8": group_lines8,
-                 "rlc_miller_chunk_2": chunk2, "rlc_miller_chunk_2_folded": chunk2f, "rlc_group_final_4": final4,
+                 "rlc_partial": rlc_partial, "rlc_duty_sum_4": duty_sum4, "rlc_group_lines": group_lines8,
+                 "rlc_miller_chunk": chunk2, "rlc_miller_chunk_folded": chunk2f, "rlc_group_final": final4,
                  "rlc_check_per_group": rlc_check_per_group,
                  "aggregate_3of4_all4": agg,
                  "unit_3of4_rlc": round(unit_3of4_rlc), "unit_3of4_each": unit_3of4,
@@ -92,8 +92,8 @@ def main():
                          {"decode_sig": decode, "hash_to_g2": hash_, "lines_sig": lines_sig,
                           "verify_quad_item": verify_quad, "verify_item_single_lane": verify,
                           "rlc_partial": rlc_partial, "rlc_duty_sum_4": duty_sum4,
-                          "rlc_group_lines_8": group_lines8, "rlc_miller_chunk_2": chunk2,
-                          "rlc_miller_chunk_2_folded": chunk2f, "rlc_group_final_4": final4,
+                          "rlc_group_lines": group_lines8, "rlc_miller_chunk": chunk2,
+                          "rlc_miller_chunk_folded": chunk2f, "rlc_group_final": final4,
                           "aggregate_3of4_all4": agg, "unit_3of4_rlc": unit_3of4_rlc,
                           "unit_3of4_each": unit_3of4, "unit_3of4_reference_schedule": unit_3of4_v1}.items()},
         "verify_hbm_bytes_per_launch": None,
