@@ -127,7 +127,7 @@ def stage_mads(wm, args):
     return {
         "decode": m["decode_sig"] * np_,
         "hash": m["hash_to_g2"] * nd,
-        "combine": m["rlc_partial"] * (np_ - nd) + m["rlc_duty_sum_4"] * nd + m["rlc_group_lines"] * ng,
+        "combine": m["rlc_partial"] * (np_ - ng) + m["rlc_duty_sum_4"] * nd + m["rlc_group_lines"] * ng,
         "h_lines": m["lines_h"] * nd,
         "verify": m["rlc_check_per_group"] * ng,
         "aggregate": m["aggregate_3of4_all4"] * nd,

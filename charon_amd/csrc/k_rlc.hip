@@ -5,7 +5,7 @@
 //
 // Every partial i of duty d signs the duty's message m_d under its own public
 // share pk_i:  e(pk_i, H(m_d)) == e(g1, s_i).  With secret 64-bit scalars r_i
-// (r = 1 for the first candidate of a duty) drawn after the inputs are fixed,
+// (r = 1 for the first candidate of a level-1 group) drawn after the inputs are fixed,
 //
 //   level 1, group of G duties:  prod_d e(P_d, H(m_d)) * e(-g1, S) == 1,
 //            P_d = sum_i r_i pk_i,  S = sum_d S_d,  S_d = sum_i r_i s_i,
@@ -58,9 +58,15 @@ __global__ void TBG_LAUNCH k_rlc_partial(DevBatch B, const G1A* pk_aff, const G1
     B.partial_status[i] = TBG_PS_ERR_PUBKEY;
     return;
   }
-  uint32_t d = B.partial_duty[i];
-  bool lead = true;  // the duty's first candidate takes r = 1
-  for (uint32_t j = B.duty_first[d]; j < i && lead; ++j)
+  // Only the first candidate of the whole level-1 GROUP takes r = 1.  (A
+  // fixed coefficient per duty would let two invalid partials of different
+  // duties in one group cancel: s_a = sig_a + D, s_b = sig_b - D.)  The duty
+  // sums S_d, P_d then carry random coefficients on all but at most one
+  // partial, which keeps the level-2 (per-duty) equations sound as well.
+  const uint32_t d = B.partial_duty[i];
+  const uint32_t d0 = (d / B.rlc_group) * B.rlc_group;
+  bool lead = true;
+  for (uint32_t j = B.duty_first[d0]; j < i && lead; ++j)
     if (rlc_usable(B, j, pk_status, n_pk)) lead = false;
   const G2A s0 = B.sig_aff[i];
   const G1A p0 = pk_aff[pid];

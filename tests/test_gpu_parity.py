@@ -217,3 +217,32 @@ def test_shared_messages_and_replay(engine):
     assert np.array_equal(again.partial_status, res.partial_status)
     assert np.array_equal(again.duty_status, res.duty_status)
     assert np.array_equal(again.agg, res.agg)
+
+
+def test_rlc_cancelling_errors_across_duties_are_rejected(engine):
+    """Two invalid partials of different duties whose errors cancel
+    (s_a = sig_a + D, s_b = sig_b - D) must not pass a level-1 group check:
+    only one candidate per GROUP may carry the fixed coefficient r = 1
+    (k_rlc.hip).  Every schedule must return the per-item verdicts."""
+    from charon_amd import tbls
+    from oracle import bls12_381 as bls
+    vecs = [dict(v) for v in load("cfg2_3of4_sample.json")[:4]]
+    assert all(v["expect"]["status"] == "ok" for v in vecs)
+    delta = bls.g2_mul(bls.G2_GEN, 0x1234567)
+    bad = {2: None, 3: None}
+    for d, sign in ((0, 1), (1, -1)):
+        v = vecs[d]
+        parts = [dict(p) for p in v["partials"]]
+        k = 0  # the first candidate of each duty
+        s = bls.g2_decompress(bytes.fromhex(parts[k]["sig"]))
+        s = bls.g2_add(s, delta if sign > 0 else bls.g2_neg(delta))
+        parts[k]["sig"] = bls.g2_compress(s).hex()
+        v["partials"] = parts
+        bad[d] = parts[k]["identifier"]
+    duties = _va_batch(engine, vecs)
+    out = tbls.verify_and_aggregate_batch(duties, engine)
+    for d, (r, v) in enumerate(zip(out, vecs)):
+        sig, signers = r
+        assert bad[d] not in signers, d
+        assert len(signers) >= v["tss"]["threshold"]
+        assert sig.raw.hex() == v["expect"]["group_sig"]

@@ -72,7 +72,8 @@ def main():
     chunk2f, _ = measure(lib.hc_stage_miller_chunk, C, 1)
     final4, _ = measure(lib.hc_stage_group_final, G // C)
     rlc_check_per_group = chunk2f + (G // C - 1) * chunk2 + final4
-    unit_3of4_rlc = (4 * decode + hash_ + lines_h + 3 * rlc_partial + duty_sum4 + group_lines8 / G
+    # every candidate but the first of each group is randomised: (4 G - 1) / G per duty
+    unit_3of4_rlc = (4 * decode + hash_ + lines_h + (4 * G - 1) / G * rlc_partial + duty_sum4 + group_lines8 / G
                      + rlc_check_per_group / G + agg)
     unit_3of4_v1 = 4 * decode + hash_ + 4 * verify + agg
     unit_3of4 = 4 * decode + hash_ + lines_h + 4 * (lines_sig + verify_quad) + agg
