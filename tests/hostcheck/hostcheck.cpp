@@ -158,7 +158,7 @@ int hc_stage_aggregate(const uint8_t* ids, const uint8_t* sigs96, int k, uint8_t
   uint32_t lam[16][8];
   if (k > 16) return -1;
   for (int i = 0; i < k; ++i)
-    if (g2_decompress(sigs96 + 96 * i, pts[i]) != DEC_OK) return -2;
+    if (g2_decompress_t<true>(sigs96 + 96 * i, pts[i]) != DEC_OK) return -2;  // k_decode_sigs' form
   uint8_t mask[16];
   for (int i = 0; i < k; ++i) {
     if (!lagrange_encode(ids, k, i, lam[i])) return -3;

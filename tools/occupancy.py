@@ -5,7 +5,8 @@ For every dispatch in the window [t_start, end] (ms from the first
 dispatch), the grid's waves are counted as resident from its start to its end
 timestamp (an upper bound: a dispatch's waves do not all run for its whole
 span).  Prints the mean number of waves demanded, the same capped at the
-machine's capacity (256 CUs x 4 SIMDs x 2 waves at <= 256 VGPRs), and each
+machine's capacity (256 CUs x 4 SIMDs = 1024 waves at one wave per SIMD,
+which is what the big kernels get: 256 VGPRs + AGPRs; 2048 at two), and each
 kernel's share of the window.
 
   python tools/occupancy.py run_kernel_trace.csv T_START_MS
@@ -36,8 +37,8 @@ def main(path, t_start_ms):
         busy[n] += w * (e - s)
     span = hi - lo
     print(f"window {span / 1e6:.1f} ms, {len(ev)} dispatches")
-    print(f"mean waves demanded {occ.mean():.0f}; capped at 2048: {np.minimum(occ, 2048).mean():.0f} "
-          f"({np.minimum(occ, 2048).mean() / 2048:.2%}); time with < 1024 waves: {(occ < 1024).mean():.1%}")
+    print(f"mean waves demanded {occ.mean():.0f}; capped at 1024 (1 wave/SIMD): {np.minimum(occ, 1024).mean():.0f} "
+          f"({np.minimum(occ, 1024).mean() / 1024:.1%}); time with < 1024 waves demanded: {(occ < 1024).mean():.1%}")
     tot = sum(busy.values())
     for n, v in busy.most_common():
         print(f"  {n:24s} {v / span:8.1f} waves avg  {v / tot:6.1%}")

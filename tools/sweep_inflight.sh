@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/sweep
 mkdir -p $O
 cd $R
-for cfg in "8 16" "10 16" "12 16" "16 16"; do
+for cfg in "8 16" "12 16" "8 16" "12 16" "12 12"; do
   set -- $cfg
   if timeout -k 10 200 python bench.py --no-cpu --inflight $1 --hw-queues $2 > $O/b_$1_$2.json 2> $O/b_$1_$2.err; then
     python -c "import json;d=json.load(open('$O/b_$1_$2.json'));print('inflight',$1,'hwq',$2,d['value'])"
