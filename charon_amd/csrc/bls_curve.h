@@ -177,13 +177,13 @@ template <class F> TBG_NI Jac<F> jac_mul_xabs(const Jac<F>& p) {
   return acc;
 }
 
-// Same schedule with the doublings inlined into the caller (call it from a
-// kernel body only: the loop body is ~90 KB of code, see bls_field.h).
+// Same schedule with the doublings and additions inlined into the caller (call
+// it from a kernel body only: the loop body is large, see bls_field.h).
 template <class F> TBG_HD Jac<F> jac_mul_xabs_in(const Jac<F>& p) {
   Jac<F> acc = p;
   for (int i = 62; i >= 0; --i) {
     acc = jac_dbl_in(acc);
-    if ((X_ABS >> i) & 1) acc = jac_add(acc, p);
+    if ((X_ABS >> i) & 1) acc = jac_add_in(acc, p);
   }
   return acc;
 }
