@@ -209,7 +209,11 @@ def main():
     from charon_amd import engine as eng
     from tools.workload import make_batch
 
-    e = eng.Engine(local, slots=max(args.inflight, 1), verify_mode=args.verify_mode, rlc_group=args.rlc_group,
+    # one GPU per rank (LOCAL_RANK); modulo the visible count so a gloo
+    # rehearsal of N ranks can share one card (identity on an 8-GPU node)
+    import torch
+    device = local % max(1, torch.cuda.device_count())
+    e = eng.Engine(device, slots=max(args.inflight, 1), verify_mode=args.verify_mode, rlc_group=args.rlc_group,
                    rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot)
     # `inflight` independent 10k-DV batches stay resident, each in its own
     # engine slot (own HBM arena + own streams); step k replays batch
@@ -255,7 +259,8 @@ def main():
     # HIP events on its stream -- the per-launch durations the roofline uses
     # (under 8-way pipelining every stage shares the CUs with 7 other batches).
     iso = e.replay(tickets[0], 1)
-    roofline_isolated, roofline = stage_rooflines(work_model(), iso, args, value)
+    # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
+    roofline_isolated, roofline = stage_rooflines(work_model(), iso, args, value / ws)
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "DV-duties/s (n verifies + 1 aggregate each)",
