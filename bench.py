@@ -186,6 +186,17 @@ def cpu_baseline(batch, seconds: float):
     return run_cpu_baseline(batch, seconds)
 
 
+def batch_exact(res, b, eng):
+    """Every partial verifies iff it was not injected, every duty with t
+    valid partials aggregates to the group signature, the others fail."""
+    if not np.array_equal(res.partial_status == eng.PS_VALID, ~b.injected):
+        return False
+    ok = res.duty_status == eng.DS_OK
+    if not np.array_equal(ok, b.expect_ok):
+        return False
+    return bool(np.array_equal(res.agg[ok], b.group_sig[ok]))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,6 +213,8 @@ def main():
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
+    ap.add_argument("--inject", type=float, default=0.0,
+                    help="fraction of partials replaced by invalid ones (side measurement; the headline is 0)")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (read at HIP init)")
     args = ap.parse_args()
 
@@ -222,15 +235,13 @@ def main():
     batches, tickets = [], []
     pcie_ms = None
     for j in range(args.inflight):
-        b = make_batch(e, args.dvs, args.t, args.n, seed=args.seed + 1000 * rank + j)
+        b = make_batch(e, args.dvs, args.t, args.n, seed=args.seed + 1000 * rank + j, inject=args.inject)
         ticket = e.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
                           duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
         first = e.collect(ticket)
         if pcie_ms is None:
             pcie_ms = e.timings()["total"]
-        ok = bool((first.partial_status == eng.PS_VALID).all() and (first.duty_status == eng.DS_OK).all()
-                  and np.array_equal(first.agg, b.group_sig))
-        if not ok:
+        if not batch_exact(first, b, eng):
             print(json.dumps({"error": "parity check failed on the bench batch"}), file=sys.stderr)
             sys.exit(2)
         batches.append(b)
@@ -247,8 +258,7 @@ def main():
     # outputs of the timed replays must still be exact
     for b, ticket in zip(batches, tickets):
         again = e.fetch(ticket, b.n_dv, b.n_dv * b.n)
-        assert np.array_equal(again.agg, b.group_sig) and (again.duty_status == eng.DS_OK).all()
-        assert (again.partial_status == eng.PS_VALID).all()
+        assert batch_exact(again, b, eng)
     b = batches[0]
 
     units = args.dvs * args.steps * ws
@@ -266,7 +276,8 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "DV-duties/s (n verifies + 1 aggregate each)",
         "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 14x28-bit limbs)",
-        "data": "synthetic (seeded shares/pubshares/signatures generated on the GPU)",
+        "data": "synthetic (seeded shares/pubshares/signatures generated on the GPU)"
+                + (f", {args.inject:.2%} injected invalid partials" if args.inject else ""),
         "config": {"workload": f"config2: {args.t}-of-{args.n}, {args.dvs} DVs x 1 attestation per GPU",
                    "partials_per_step_per_gpu": args.dvs * args.n, "parallelism": f"shard{ws}",
                    "inflight_batches": args.inflight, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
