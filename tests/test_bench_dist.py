@@ -65,3 +65,29 @@ def test_roofline_fields_from_work_model():
     assert abs(stage["achieved"] - stage["algorithmic_mads_per_launch"] / 11.2e-3 / 1e12) < 1e-2
     assert abs(pipe["achieved"] - 1.0e6 * wm["mads"]["unit_3of4_rlc"] / 1e12) < 1e-2
     assert 0 < pipe["frac"] < 1
+
+
+def test_batch_exact_follows_injection():
+    """bench.py's exactness check under --inject (no GPU): a partial must
+    verify iff it was not injected, a duty aggregates iff it kept t valid
+    partials, and only those duties' aggregates are compared."""
+    import types
+    import numpy as np
+    import bench
+    eng = types.SimpleNamespace(PS_VALID=1, DS_OK=0)
+    injected = np.array([False, True, False, False, True, True, False, False])  # 2 duties x 4
+    expect_ok = np.array([True, False])                                      # t = 3
+    group_sig = np.arange(2 * 96, dtype=np.uint8).reshape(2, 96)
+    b = types.SimpleNamespace(injected=injected, expect_ok=expect_ok, group_sig=group_sig)
+    agg = group_sig.copy()
+    agg[1] = 0  # a failed duty's aggregate is not compared
+    good = types.SimpleNamespace(partial_status=np.where(injected, 0, 1).astype(np.int32),
+                                 duty_status=np.array([0, 3], dtype=np.int32), agg=agg)
+    assert bench.batch_exact(good, b, eng)
+    flipped = types.SimpleNamespace(**{**vars(good), "partial_status": np.ones(8, dtype=np.int32)})
+    assert not bench.batch_exact(flipped, b, eng)
+    wrong_duty = types.SimpleNamespace(**{**vars(good), "duty_status": np.zeros(2, dtype=np.int32)})
+    assert not bench.batch_exact(wrong_duty, b, eng)
+    bad_agg = agg.copy()
+    bad_agg[0, 5] ^= 1
+    assert not bench.batch_exact(types.SimpleNamespace(**{**vars(good), "agg": bad_agg}), b, eng)
