@@ -122,7 +122,17 @@ TBG_NI bool lagrange_encode(const uint8_t* ids, int k, int me, uint32_t (&w)[8])
 
 // sum_j coeff_j * P_j over the participants (mask[j] != 0), coefficients as
 // encoded by lagrange_encode.  pts / lam are indexed j = 0..count-1.
-TBG_NI G2J tss_combine(const G2A* pts, const uint32_t* lam, const uint8_t* mask, int count) {
+// defer_D != nullptr: an integer-mode sum with denominator D > 1 is returned
+// before the [1/D] multiplication and *defer_D = D (else *defer_D = 1); the
+// caller finishes it with tss_div_den.
+TBG_HD G2J tss_div_den(const G2J& acc, uint64_t D) {
+  uint32_t dw[8];
+  fr_to_words(fr_inv(fr_from_u64(D)), dw);
+  return jac_mul_words(acc, dw, 255);
+}
+TBG_NI G2J tss_combine(const G2A* pts, const uint32_t* lam, const uint8_t* mask, int count,
+                       uint64_t* defer_D = nullptr) {
+  if (defer_D) *defer_D = 1;
   int first = -1;
   for (int j = 0; j < count; ++j)
     if (mask[j]) { first = j; break; }
@@ -149,9 +159,8 @@ TBG_NI G2J tss_combine(const G2A* pts, const uint32_t* lam, const uint8_t* mask,
     }
     uint64_t D = (uint64_t)lam[8 * first + 2] | ((uint64_t)lam[8 * first + 3] << 32);
     if (D > 1) {
-      uint32_t dw[8];
-      fr_to_words(fr_inv(fr_from_u64(D)), dw);
-      acc = jac_mul_words(acc, dw, 255);
+      if (defer_D) *defer_D = D;
+      else acc = tss_div_den(acc, D);
     }
     return acc;
   }

@@ -25,6 +25,22 @@ __global__ void TBG_LAUNCH k_lagrange(DevBatch B) {
   for (int j = 0; j < 8; ++j) w[j] = lw[j];
 }
 
+// Affine conversion, compression and status of a finished sum.
+__device__ void agg_emit(const DevBatch& B, uint32_t d, const G2J& acc) {
+  uint8_t* out = B.agg + 96ull * d;
+  G2A a;
+  if (!jac_to_aff(acc, a)) { B.duty_status[d] = TBG_DS_AGG_IDENTITY; return; }
+  uint8_t enc[96];
+  g2_compress(a, false, enc);
+  for (int j = 0; j < 96; ++j) out[j] = enc[j];
+  B.duty_status[d] = TBG_DS_OK;
+}
+
+// Duties whose participants' integer Lagrange coefficients share a
+// denominator D > 1 (a partial missing from the middle of the id range,
+// e.g. ids {1,2,4}: lambda_1 = 8/3) need a 255-bit [1/D] multiplication.
+// Inline, one such duty makes its whole 64-lane wave pay that loop; they are
+// listed here instead and finished by k_aggregate_finish in uniform waves.
 __global__ void TBG_LAUNCH k_aggregate(DevBatch B) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= B.n_duties) return;
@@ -65,13 +81,26 @@ __global__ void TBG_LAUNCH k_aggregate(DevBatch B) {
   }
   uint8_t mask[256];
   for (uint32_t j = first; j < last; ++j) mask[j - first] = participates(B.op, B.partial_status[j]) ? 1 : 0;
-  G2J acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n);
-  G2A a;
-  if (!jac_to_aff(acc, a)) { B.duty_status[d] = TBG_DS_AGG_IDENTITY; return; }
-  uint8_t enc[96];
-  g2_compress(a, false, enc);
-  for (int j = 0; j < 96; ++j) out[j] = enc[j];
-  B.duty_status[d] = TBG_DS_OK;
+  uint64_t D = 1;
+  G2J acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
+  if (D > 1) {
+    B.agg_acc[d] = acc;
+    B.agg_list[atomicAdd(&B.counters[CNT_AGG], 1u)] = d;
+    return;
+  }
+  agg_emit(B, d, acc);
+}
+
+__global__ void TBG_LAUNCH k_aggregate_finish(DevBatch B) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= B.counters[CNT_AGG]) return;
+  uint32_t d = B.agg_list[k];
+  uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
+  uint32_t j = first;
+  while (j < last && !participates(B.op, B.partial_status[j])) ++j;
+  const uint32_t* w = B.lam + 8ull * j;  // listed duties have a participant (k >= 2)
+  uint64_t D = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  agg_emit(B, d, tss_div_den(B.agg_acc[d], D));
 }
 
 void launch_lagrange(const DevBatch& B, hipStream_t st) {
@@ -79,6 +108,9 @@ void launch_lagrange(const DevBatch& B, hipStream_t st) {
 }
 void launch_aggregate(const DevBatch& B, hipStream_t st) {
   if (B.n_duties) TBG_KLAUNCH(k_aggregate, grid_for(B.n_duties), dim3(kBlock), st, B);
+}
+void launch_aggregate_finish(const DevBatch& B, hipStream_t st) {
+  if (B.n_duties) TBG_KLAUNCH(k_aggregate_finish, grid_for(B.n_duties), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

@@ -287,6 +287,7 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   if (B.op != TBG_OP_VERIFY) launch_lagrange(B, st);
   HIP_TRY(hipEventRecord(ev[8], st));
   launch_aggregate(B, st);
+  if (B.op != TBG_OP_VERIFY) launch_aggregate_finish(B, st);
   HIP_TRY(hipEventRecord(ev[9], st));
   HIP_TRY(hipGetLastError());
   return TBG_OK;
@@ -381,6 +382,8 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   size_t w_dvl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_dvlines = sec(G > 1 ? 4ull * LINES_WORDS * nd : 0);
   size_t w_pl = sec(verify ? 4ull * np : 0);
+  size_t w_aacc = sec(b->op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
+  size_t w_alist = sec(b->op != TBG_OP_VERIFY ? 4ull * nd : 0);
   size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
   size_t w_pst = sec(4ull * np);
   size_t w_dst = sec(4ull * nd);
@@ -471,6 +474,8 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   B.partial_status = (int32_t*)(dw + w_pst);
   B.duty_status = (int32_t*)(dw + w_dst);
   B.agg = dw + w_agg;
+  B.agg_acc = (G2J*)(dw + w_aacc);
+  B.agg_list = (uint32_t*)(dw + w_alist);
 
   hipStream_t st = s->st;
   // The resident pubkey table may have been (re)loaded on the utility stream.

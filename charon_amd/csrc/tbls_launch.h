@@ -55,6 +55,9 @@ struct DevBatch {
   uint32_t* dv_list;      // [n_duties] level-2 duties
   uint32_t* dv_lines;     // [n_duties][LINES_WORDS] lines of S_d, by level-2 list position
   uint32_t* part_list;    // [n_partials] level-3 partials (sig_lines by list position)
+  // recombination (k_aggregate.hip)
+  G2J* agg_acc;           // [n_duties] integer-coefficient sums awaiting [1/D] (listed duties only)
+  uint32_t* agg_list;     // [n_duties] duties whose Lagrange denominator D > 1
   // outputs
   int32_t* partial_status;
   int32_t* duty_status;
@@ -63,7 +66,7 @@ struct DevBatch {
 
 enum RlcState : int32_t { RLC_NONE = 0, RLC_COMBINED = 1, RLC_EACH = 2 };
 enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3 };
-enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_WORDS = 4 };
+enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_WORDS = 4 };
 
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {
@@ -90,6 +93,7 @@ void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff
 void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
 void launch_lagrange(const DevBatch& B, hipStream_t st);
 void launch_aggregate(const DevBatch& B, hipStream_t st);
+void launch_aggregate_finish(const DevBatch& B, hipStream_t st);
 void launch_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* pk48, hipStream_t st);
 void launch_sign(const uint8_t* sk32, const uint32_t* item_msg, uint32_t n, const G2A* h_aff, const int32_t* h_status,
                  uint8_t* sig96, hipStream_t st);
