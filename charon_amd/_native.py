@@ -37,7 +37,8 @@ def is_stale():
     return any(os.path.getmtime(s) > t for s in sources())
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(), out: str | None = None) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(), out: str | None = None,
+          extra_flags=(), link_flags=()) -> str:
     """Compile the engine for gfx950: every csrc/*.hip translation unit in
     parallel (hipcc -c), then link libtbls_gpu.so.  `defines` / `out` build a
     tuning variant elsewhere (tools/ab_variants.py)."""
@@ -47,13 +48,25 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     from concurrent.futures import ThreadPoolExecutor
     hipcc = _hipcc()
     units = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
-    objdir = os.path.join(PKG, "build_obj", os.path.basename(target).replace(".so", ""))
+    # one object directory per output (variants never share the product's objects)
+    tag = os.path.basename(target).replace(".so", "")
+    if os.path.abspath(target) != LIB_PATH:
+        tag = os.path.basename(os.path.dirname(os.path.abspath(target))) + "_" + tag
+    objdir = os.path.join(PKG, "build_obj", tag)
     os.makedirs(objdir, exist_ok=True)
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed", "-Wno-unused-result", "-Wno-unused-value"]
-    flags += ["-D" + d for d in defines]
+    flags += ["-D" + d for d in defines] + list(extra_flags)
+
+    headers = [s for s in sources() if s.endswith(".h")]
+    stamp = os.path.join(objdir, "flags.txt")
+    same_flags = os.path.exists(stamp) and open(stamp).read() == " ".join(flags)
 
     def compile_unit(u):
         obj = os.path.join(objdir, u.replace(".hip", ".o"))
+        if same_flags and not force and os.path.exists(obj):
+            t = os.path.getmtime(obj)
+            if all(os.path.getmtime(d) < t for d in headers + [os.path.join(CSRC, u)]):
+                return obj  # up to date (incremental rebuild)
         cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, u), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -65,7 +78,9 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
         objs = list(ex.map(compile_unit, units))
     for obj in objs:
         check_return_address(obj)
-    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", target + ".tmp"]
+    with open(stamp, "w") as f:
+        f.write(" ".join(flags))
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + list(link_flags) + objs + ["-o", target + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
@@ -82,8 +97,10 @@ def check_return_address(obj: str) -> None:
     and the kernel never finishes (observed on gfx950).  Kernels use a free
     SGPR pair and are not affected."""
     llvm = "/opt/rocm/llvm/bin"
-    if not os.path.exists(os.path.join(llvm, "llvm-objdump")):
-        return
+    for tool in ("llvm-objdump", "llvm-objcopy", "clang-offload-bundler"):
+        if not os.path.exists(os.path.join(llvm, tool)):
+            # fail closed: this guard stands between a known GPU hang and the box
+            raise RuntimeError(f"{llvm}/{tool} is missing: cannot run the return-address check on {obj}")
     import re
     import tempfile
     heads = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-h", obj], capture_output=True, text=True).stdout
@@ -158,6 +175,18 @@ SIGNATURES = {
     "tbg_sk_to_pk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     "tbg_sign": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "tbg_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "tbg_multi_init": (ctypes.c_int, [ctypes.POINTER(TbgConfig), ctypes.c_void_p, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_void_p)]),
+    "tbg_multi_destroy": (None, [ctypes.c_void_p]),
+    "tbg_multi_size": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "tbg_multi_context": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint32]),
+    "tbg_multi_load_pubkeys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                              ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p]),
+    "tbg_multi_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TbgBatch), ctypes.POINTER(ctypes.c_uint64)]),
+    "tbg_multi_collect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int]),
+    "tbg_multi_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -42,48 +42,58 @@ TBG_HD uint64_t gcd_u64(uint64_t a, uint64_t b) {
 
 TBG_HD int bitlen_u64(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 
+// Reduced fraction lambda_j(0) = (neg ? -a : a) / b of participant j, b > 0.
+// Returns 1, 0 when the products would overflow 62 bits, -1 on duplicates.
+TBG_HD int lagrange_frac(const uint8_t* ids, int k, int j, uint64_t& a, uint64_t& b, int& neg) {
+  uint64_t num = 1, den = 1;
+  int bits = 0;
+  neg = 0;
+  for (int m = 0; m < k; ++m) {
+    if (m == j) continue;
+    int64_t d = (int64_t)ids[m] - (int64_t)ids[j];
+    if (d == 0) return -1;
+    if (d < 0) { neg ^= 1; d = -d; }
+    bits += bitlen_u64(ids[m]) + bitlen_u64((uint64_t)d);
+    if (bits > 62) return 0;
+    num *= ids[m];
+    den *= (uint64_t)d;
+  }
+  if (num == 0) {
+    a = 0;
+    b = 1;
+  } else {
+    uint64_t g = gcd_u64(num, den);
+    a = num / g;
+    b = den / g;
+  }
+  return 1;
+}
+
 // Returns 1 on success (N, D set), 0 when the integers would overflow (use
-// the mod-r path), -1 on duplicate identifiers.
+// the mod-r path), -1 on duplicate identifiers.  The integer / mod-r choice
+// is a property of the participant SET, never of i: every participant of a
+// duty must get its coefficient in the same encoding, because tss_combine
+// reads the mode of the first one for all of them.  So the overflow test runs
+// over every j (pass 2), not only over i.
 TBG_NI int lagrange_int(const uint8_t* ids, int k, int i, int64_t& N, uint64_t& D) {
-  // reduced fractions a_j / b_j (b_j > 0) for every participant j
   uint64_t lcm = 1;
-  int64_t ai = 0;
-  uint64_t bi = 1;
-  for (int j = 0; j < k; ++j) {
-    uint64_t num = 1, den = 1;
-    int neg = 0, bits = 0;
-    for (int m = 0; m < k; ++m) {
-      if (m == j) continue;
-      int64_t d = (int64_t)ids[m] - (int64_t)ids[j];
-      if (d == 0) return -1;
-      if (d < 0) { neg ^= 1; d = -d; }
-      bits += bitlen_u64(ids[m]) + bitlen_u64((uint64_t)d);
-      if (bits > 62) return 0;
-      num *= ids[m];
-      den *= (uint64_t)d;
-    }
-    uint64_t a, b;
-    if (num == 0) {
-      a = 0;
-      b = 1;
-    } else {
-      uint64_t g = gcd_u64(num, den);
-      a = num / g;
-      b = den / g;
-    }
-    uint64_t g2 = gcd_u64(lcm, b);
-    uint64_t q = b / g2;
+  uint64_t a, b;
+  int neg;
+  for (int j = 0; j < k; ++j) {  // pass 1: D = lcm of the reduced denominators
+    int r = lagrange_frac(ids, k, j, a, b, neg);
+    if (r <= 0) return r;
+    uint64_t q = b / gcd_u64(lcm, b);
     if (bitlen_u64(lcm) + bitlen_u64(q) > 62) return 0;
     lcm *= q;
-    if (j == i) {
-      ai = neg ? -(int64_t)a : (int64_t)a;
-      bi = b;
-    }
   }
-  uint64_t scale = lcm / bi;
-  uint64_t mag = (uint64_t)(ai < 0 ? -ai : ai);
-  if (bitlen_u64(mag) + bitlen_u64(scale) > 62) return 0;
-  N = ai * (int64_t)scale;
+  int64_t ni = 0;
+  for (int j = 0; j < k; ++j) {  // pass 2: every N_j = a_j D / b_j must fit
+    lagrange_frac(ids, k, j, a, b, neg);
+    uint64_t scale = lcm / b;
+    if (bitlen_u64(a) + bitlen_u64(scale) > 62) return 0;
+    if (j == i) ni = neg ? -(int64_t)(a * scale) : (int64_t)(a * scale);
+  }
+  N = ni;
   D = lcm;
   return 1;
 }

@@ -39,7 +39,7 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct Slot {
   bool busy = false;
-  bool done_collected = true;
+  bool collecting = false;  // a blocking tbg_collect waits on `done` outside the context mutex
   tbg_ticket ticket = 0;
   uint32_t op = 0, n_duties = 0, n_partials = 0, n_msgs = 0;
   // pinned host staging
@@ -72,6 +72,7 @@ struct tbg_ctx {
   G1A* d_xpk = nullptr;  // [x] pk per entry (k_decode_pubkeys)
   int32_t* d_pk_status = nullptr;
   uint32_t n_pk = 0, cap_pk = 0;
+  std::vector<void*> retired;  // outgrown pubkey tables (see tbg_load_pubkeys)
   std::vector<Slot> slots;
   tbg_ticket next_ticket = 1;
   float last_ms[8] = {};
@@ -159,6 +160,11 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // overlap on the GPU (one batch's latency-bound stages fill the CUs the
   // other leaves idle).
   uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 3;
+  if (nslots > TBG_MAX_SLOTS || (cfg && cfg->streams_per_slot > 2)) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return TBG_E_INVALID_ARG;
+  }
   c->slots.resize(nslots);
   // One stream per slot by default: the HIP runtime maps streams onto a
   // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), so concurrency
@@ -200,6 +206,7 @@ void tbg_destroy(tbg_ctx* c) {
   if (c->d_pk) hipFree(c->d_pk);
   if (c->d_xpk) hipFree(c->d_xpk);
   if (c->d_pk_status) hipFree(c->d_pk_status);
+  for (void* p : c->retired) hipFree(p);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -226,13 +233,13 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
       HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    for (auto& sl : c->slots) {  // in-flight batches may still read the old table
-      HIP_TRY(hipStreamSynchronize(sl.st));
-      HIP_TRY(hipStreamSynchronize(sl.st2));
-    }
-    if (c->d_pk) hipFree(c->d_pk);
-    if (c->d_xpk) hipFree(c->d_xpk);
-    if (c->d_pk_status) hipFree(c->d_pk_status);
+    // Batches already in flight captured the old table's address in their
+    // kernel arguments: retire it (freed by tbg_destroy) instead of waiting
+    // for every slot.  Growth is geometric, so retired tables stay below 2x
+    // the final one.
+    if (c->d_pk) c->retired.push_back(c->d_pk);
+    if (c->d_xpk) c->retired.push_back(c->d_xpk);
+    if (c->d_pk_status) c->retired.push_back(c->d_pk_status);
     c->d_pk = npk;
     c->d_xpk = nxpk;
     c->d_pk_status = nst;
@@ -499,7 +506,7 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   return TBG_OK;
 }
 
-int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg, int block) {
+int tbg_poll(tbg_ctx* c, tbg_ticket t) {
   if (!c) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   Slot* s = nullptr;
@@ -507,11 +514,35 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     if (x.busy && x.ticket == t) { s = &x; break; }
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
-  if (!block) {
-    hipError_t q = hipEventQuery(s->done);
-    if (q == hipErrorNotReady) return TBG_E_PENDING;
-    if (q != hipSuccess) { s->busy = false; return TBG_E_DEVICE; }
-  } else if (hipEventSynchronize(s->done) != hipSuccess) {
+  hipError_t q = hipEventQuery(s->done);
+  if (q == hipErrorNotReady) return TBG_E_PENDING;
+  return q == hipSuccess ? TBG_OK : TBG_E_DEVICE;
+}
+
+int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg, int block) {
+  if (!c) return TBG_E_INVALID_ARG;
+  std::unique_lock<std::mutex> lk(c->mu);
+  Slot* s = nullptr;
+  for (auto& x : c->slots)
+    if (x.busy && x.ticket == t) { s = &x; break; }
+  if (!s || s->collecting) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  hipError_t q = hipEventQuery(s->done);
+  if (q == hipErrorNotReady) {
+    if (!block) return TBG_E_PENDING;
+    // Wait without the context mutex: other threads keep submitting and
+    // polling meanwhile.  `collecting` keeps this slot (busy) out of every
+    // other submit / collect until the wait is over.
+    s->collecting = true;
+    hipEvent_t done = s->done;
+    int dev = c->device;
+    lk.unlock();
+    (void)hipSetDevice(dev);  // the HIP current device is per thread
+    q = hipEventSynchronize(done);
+    lk.lock();
+    s->collecting = false;
+  }
+  if (q != hipSuccess) {
     s->busy = false;
     return TBG_E_DEVICE;
   }

@@ -1,0 +1,277 @@
+// libtbls_gpu.so, multi-device part: one process driving several GPUs
+// (BASELINE config 4: 1 M DV-duties over 8 x MI355X with a host gather).
+//
+// A multi-context owns one single-device context per entry of devices[].
+// Duties are independent (no cross-device math), so a batch is
+// cut into contiguous duty ranges of about equal partial counts; every range
+// becomes a sub-batch that shares the caller's arrays by pointer offset (only
+// duty_first is rebased and the messages a range uses are re-indexed), and the
+// sub-batches are packed and submitted concurrently, one host thread per
+// context.  Collection writes each shard's statuses and aggregates straight
+// into the caller's arrays at the shard's offsets, so the gather is the
+// per-DV loop order of core/parsigex/parsigex.go:101-107 and
+// core/parsigdb/memory.go:96-134 -> core/sigagg/sigagg.go:53-103 by
+// construction.  Host code only.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+#include "../../include/tbls_gpu.h"
+
+namespace {
+
+struct Shard {
+  uint32_t ctx = 0;
+  tbg_ticket ticket = 0;
+  uint32_t d0 = 0, d1 = 0, p0 = 0, p1 = 0;
+};
+
+struct Job {
+  std::vector<Shard> shards;
+  std::vector<uint32_t> duty_lo;  // [size + 1] cut points (empty shards included)
+  bool collecting = false;
+};
+
+// Sub-batch of duties [d0, d1): pointers into the caller's arrays plus the
+// few rebased index arrays it owns.
+struct SubBatch {
+  tbg_batch b{};
+  std::vector<uint32_t> duty_first, duty_msg, msg_off;
+  std::vector<uint8_t> msgs;
+
+  void build(const tbg_batch& src, uint32_t d0, uint32_t d1) {
+    const uint32_t p0 = src.duty_first[d0], p1 = src.duty_first[d1];
+    b = src;
+    b.n_duties = d1 - d0;
+    b.n_partials = p1 - p0;
+    duty_first.resize(b.n_duties + 1);
+    for (uint32_t i = 0; i <= b.n_duties; ++i) duty_first[i] = src.duty_first[d0 + i] - p0;
+    b.duty_first = duty_first.data();
+    b.sigs = src.sigs ? src.sigs + 96ull * p0 : nullptr;
+    b.identifiers = src.identifiers ? src.identifiers + p0 : nullptr;
+    b.pubkey_ids = src.pubkey_ids ? src.pubkey_ids + p0 : nullptr;
+    b.duty_threshold = src.duty_threshold ? src.duty_threshold + d0 : nullptr;
+    if (src.op == TBG_OP_AGGREGATE) return;
+    // Messages: a contiguous increasing run (one message per duty, the usual
+    // attestation batch) is shared by offset; anything else (committees that
+    // share a signing root) is re-indexed to the messages this range uses.
+    bool run = true;
+    for (uint32_t d = d0 + 1; d < d1 && run; ++d) run = src.duty_msg[d] == src.duty_msg[d - 1] + 1;
+    duty_msg.resize(b.n_duties);
+    if (run) {
+      const uint32_t m0 = src.duty_msg[d0], nm = d1 - d0;
+      msg_off.resize(nm + 1);
+      for (uint32_t i = 0; i <= nm; ++i) msg_off[i] = src.msg_off[m0 + i] - src.msg_off[m0];
+      for (uint32_t i = 0; i < nm; ++i) duty_msg[i] = i;
+      b.msgs = src.msgs ? src.msgs + src.msg_off[m0] : nullptr;
+      b.n_msgs = nm;
+    } else {
+      std::unordered_map<uint32_t, uint32_t> local;
+      local.reserve(2 * (size_t)b.n_duties);
+      msg_off.assign(1, 0);
+      for (uint32_t d = d0; d < d1; ++d) {
+        const uint32_t m = src.duty_msg[d];
+        auto it = local.find(m);
+        if (it == local.end()) {
+          it = local.emplace(m, (uint32_t)local.size()).first;
+          const uint32_t len = src.msg_off[m + 1] - src.msg_off[m];
+          msgs.insert(msgs.end(), src.msgs + src.msg_off[m], src.msgs + src.msg_off[m] + len);
+          msg_off.push_back((uint32_t)msgs.size());
+        }
+        duty_msg[d - d0] = it->second;
+      }
+      if (msgs.empty()) msgs.push_back(0);  // a valid pointer for empty messages
+      b.msgs = msgs.data();
+      b.n_msgs = (uint32_t)local.size();
+    }
+    b.msg_off = msg_off.data();
+    b.duty_msg = duty_msg.data();
+  }
+};
+
+// What the per-context validate() checks, for the parts the split relies on.
+int validate_split(const tbg_batch* b) {
+  if (!b || b->n_duties == 0 || !b->duty_first) return TBG_E_INVALID_ARG;
+  if (b->op < TBG_OP_VERIFY || b->op > TBG_OP_VERIFY_AGGREGATE) return TBG_E_INVALID_ARG;
+  if (b->duty_first[0] != 0 || b->duty_first[b->n_duties] != b->n_partials) return TBG_E_INVALID_ARG;
+  for (uint32_t d = 0; d < b->n_duties; ++d)
+    if (b->duty_first[d + 1] < b->duty_first[d]) return TBG_E_INVALID_ARG;
+  if (b->op != TBG_OP_AGGREGATE) {
+    if (!b->msg_off || !b->duty_msg || b->n_msgs == 0) return TBG_E_INVALID_ARG;
+    if (b->msg_off[0] != 0) return TBG_E_INVALID_ARG;
+    for (uint32_t m = 0; m < b->n_msgs; ++m)
+      if (b->msg_off[m + 1] < b->msg_off[m]) return TBG_E_INVALID_ARG;
+    if (b->msg_off[b->n_msgs] && !b->msgs) return TBG_E_INVALID_ARG;
+    for (uint32_t d = 0; d < b->n_duties; ++d)
+      if (b->duty_msg[d] >= b->n_msgs) return TBG_E_INVALID_ARG;
+  }
+  return TBG_OK;
+}
+
+// Run fn(i) for i in [0, n) on n threads (i = 0 on the caller's thread).
+template <class F>
+void parallel_for(uint32_t n, F fn) {
+  std::vector<std::thread> th;
+  th.reserve(n ? n - 1 : 0);
+  for (uint32_t i = 1; i < n; ++i) th.emplace_back(fn, i);
+  if (n) fn(0);
+  for (auto& t : th) t.join();
+}
+
+}  // namespace
+
+struct tbg_multi {
+  std::vector<tbg_ctx*> ctx;
+  std::mutex mu;
+  std::unordered_map<tbg_ticket, Job> jobs;
+  tbg_ticket next_ticket = 1;
+};
+
+extern "C" {
+
+int tbg_multi_init(const tbg_config* cfg, const int32_t* devices, uint32_t n_devices, tbg_multi** out) {
+  if (!out || !devices || n_devices == 0 || n_devices > 64) return TBG_E_INVALID_ARG;
+  *out = nullptr;
+  tbg_multi* m = new (std::nothrow) tbg_multi();
+  if (!m) return TBG_E_OOM;
+  tbg_config c{};
+  if (cfg) c = *cfg;
+  for (uint32_t i = 0; i < n_devices; ++i) {
+    c.device = devices[i];
+    tbg_ctx* x = nullptr;
+    int rc = tbg_init(&c, &x);
+    if (rc != TBG_OK) {
+      tbg_multi_destroy(m);
+      return rc;
+    }
+    m->ctx.push_back(x);
+  }
+  *out = m;
+  return TBG_OK;
+}
+
+void tbg_multi_destroy(tbg_multi* m) {
+  if (!m) return;
+  for (auto* x : m->ctx) tbg_destroy(x);
+  delete m;
+}
+
+uint32_t tbg_multi_size(const tbg_multi* m) { return m ? (uint32_t)m->ctx.size() : 0; }
+
+tbg_ctx* tbg_multi_context(tbg_multi* m, uint32_t i) { return (m && i < m->ctx.size()) ? m->ctx[i] : nullptr; }
+
+int tbg_multi_load_pubkeys(tbg_multi* m, const uint8_t* pk48, uint32_t count, uint32_t* first_id, int32_t* status) {
+  if (!m || (count && !pk48)) return TBG_E_INVALID_ARG;
+  const uint32_t n = (uint32_t)m->ctx.size();
+  std::vector<int> rc(n, TBG_OK);
+  std::vector<uint32_t> first(n, 0);
+  // The same table decoded on every device (in parallel); the status of
+  // context 0 is reported (every device computes the same one).
+  parallel_for(n, [&](uint32_t i) { rc[i] = tbg_load_pubkeys(m->ctx[i], pk48, count, &first[i], i == 0 ? status : nullptr); });
+  for (uint32_t i = 0; i < n; ++i)
+    if (rc[i] != TBG_OK) return rc[i];
+  for (uint32_t i = 1; i < n; ++i)
+    if (first[i] != first[0]) return TBG_E_INVALID_ARG;  // a context was loaded outside the multi-context
+  if (first_id) *first_id = first[0];
+  return TBG_OK;
+}
+
+int tbg_multi_submit(tbg_multi* m, const tbg_batch* b, tbg_ticket* ticket) {
+  if (!m || !ticket) return TBG_E_INVALID_ARG;
+  int rc = validate_split(b);
+  if (rc != TBG_OK) return rc;
+  const uint32_t n = (uint32_t)m->ctx.size(), nd = b->n_duties, np = b->n_partials;
+  // Cut points: shard i starts at the first duty whose first partial is at
+  // or past i * np / n (duties with many partials are never split); with no
+  // partials at all, duties are split evenly.
+  Job job;
+  job.duty_lo.resize(n + 1);
+  job.duty_lo[0] = 0;
+  job.duty_lo[n] = nd;
+  for (uint32_t i = 1; i < n; ++i) {
+    uint32_t d;
+    if (np) {
+      const uint32_t target = (uint32_t)((uint64_t)np * i / n);
+      d = (uint32_t)(std::lower_bound(b->duty_first, b->duty_first + nd + 1, target) - b->duty_first);
+    } else {
+      d = (uint32_t)((uint64_t)nd * i / n);
+    }
+    job.duty_lo[i] = std::max(job.duty_lo[i - 1], std::min(d, nd));
+  }
+  std::vector<uint32_t> use;
+  for (uint32_t i = 0; i < n; ++i)
+    if (job.duty_lo[i + 1] > job.duty_lo[i]) use.push_back(i);
+  std::vector<int> src(use.size(), TBG_OK);
+  job.shards.resize(use.size());
+  parallel_for((uint32_t)use.size(), [&](uint32_t k) {
+    const uint32_t i = use[k];
+    Shard& s = job.shards[k];
+    s.ctx = i;
+    s.d0 = job.duty_lo[i];
+    s.d1 = job.duty_lo[i + 1];
+    s.p0 = b->duty_first[s.d0];
+    s.p1 = b->duty_first[s.d1];
+    SubBatch sb;
+    sb.build(*b, s.d0, s.d1);
+    src[k] = tbg_submit(m->ctx[i], &sb.b, &s.ticket);  // copies everything it needs
+  });
+  for (size_t k = 0; k < src.size(); ++k) {
+    if (src[k] == TBG_OK) continue;
+    // undo: drain the shards that did start, then report the first error
+    for (size_t j = 0; j < src.size(); ++j)
+      if (src[j] == TBG_OK) tbg_collect(m->ctx[job.shards[j].ctx], job.shards[j].ticket, nullptr, nullptr, nullptr, 1);
+    return src[k];
+  }
+  std::lock_guard<std::mutex> lk(m->mu);
+  *ticket = m->next_ticket++;
+  m->jobs.emplace(*ticket, std::move(job));
+  return TBG_OK;
+}
+
+int tbg_multi_collect(tbg_multi* m, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg, int block) {
+  if (!m) return TBG_E_INVALID_ARG;
+  Job* job = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    auto it = m->jobs.find(t);
+    if (it == m->jobs.end() || it->second.collecting) return TBG_E_TICKET;
+    job = &it->second;
+    if (!block) {
+      for (const Shard& s : job->shards) {
+        int q = tbg_poll(m->ctx[s.ctx], s.ticket);
+        if (q == TBG_E_PENDING) return TBG_E_PENDING;
+      }
+    }
+    job->collecting = true;  // the map node stays put: unordered_map references are stable
+  }
+  // Every shard's wait and copy-out runs on its own thread, straight into the
+  // caller's arrays at the shard's offsets (caller order by construction).
+  std::vector<int> rc(job->shards.size(), TBG_OK);
+  parallel_for((uint32_t)job->shards.size(), [&](uint32_t k) {
+    const Shard& s = job->shards[k];
+    rc[k] = tbg_collect(m->ctx[s.ctx], s.ticket, pst ? pst + s.p0 : nullptr, dst ? dst + s.d0 : nullptr,
+                        agg ? agg + 96ull * s.d0 : nullptr, 1);
+  });
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->jobs.erase(t);
+  }
+  for (int r : rc)
+    if (r != TBG_OK) return r;
+  return TBG_OK;
+}
+
+int tbg_multi_layout(tbg_multi* m, tbg_ticket t, uint32_t* duty_lo) {
+  if (!m || !duty_lo) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(m->mu);
+  auto it = m->jobs.find(t);
+  if (it == m->jobs.end()) return TBG_E_TICKET;
+  std::copy(it->second.duty_lo.begin(), it->second.duty_lo.end(), duty_lo);
+  return TBG_OK;
+}
+
+}  // extern "C"

@@ -157,6 +157,14 @@ class Engine:
     def run(self, op, duty_first, sigs, identifiers, **kw) -> BatchResult:
         return self.collect(self.submit(op, duty_first, sigs, identifiers, **kw))
 
+    def poll(self, ticket) -> bool:
+        """True once the batch has finished (nothing is consumed)."""
+        rc = self._lib.tbg_poll(self._h, ticket)
+        if rc == E_PENDING:
+            return False
+        self._check(rc, "tbg_poll")
+        return True
+
     def replay(self, ticket, iters=1):
         """Re-run a collected batch's kernel chain on its resident inputs."""
         ms = np.zeros(8, dtype=np.float32)
@@ -203,6 +211,86 @@ class Engine:
         self._check(self._lib.tbg_sign(self._h, _ptr(a), a.shape[0], _ptr(data), _ptr(off), len(off) - 1, _ptr(im),
                                        _ptr(out)), "tbg_sign")
         return out
+
+
+class MultiEngine:
+    """One process, several GPUs (tbg_multi_*): batches are cut into
+    contiguous duty ranges, one per context, submitted concurrently and
+    gathered back into caller order.  ``devices`` may repeat an ordinal
+    (several contexts on one GPU)."""
+
+    def __init__(self, devices, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0, rlc_seed: int = 0,
+                 rlc_chunk: int = 0, streams_per_slot: int = 0):
+        self._lib = _native.load()
+        cfg = _native.TbgConfig(device=0, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
+                                verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
+                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot)
+        devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
+        h = ctypes.c_void_p()
+        rc = self._lib.tbg_multi_init(ctypes.byref(cfg), _ptr(devs), len(devs), ctypes.byref(h))
+        if rc != 0:
+            raise EngineError(f"tbg_multi_init: {self._lib.tbg_strerror(rc).decode()} ({rc})")
+        self._h = h
+        self.devices = devs.tolist()
+        self.uid = next(_serial)
+        self._keep = {}
+
+    _check = Engine._check
+    _batch = Engine._batch
+
+    @property
+    def size(self) -> int:
+        return self._lib.tbg_multi_size(self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.tbg_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_pubkeys(self, pk48) -> tuple[int, np.ndarray]:
+        a = _u8(pk48, 48)
+        n = a.shape[0]
+        first = ctypes.c_uint32()
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self._lib.tbg_multi_load_pubkeys(self._h, _ptr(a), n, ctypes.byref(first), _ptr(st)),
+                    "tbg_multi_load_pubkeys")
+        return first.value, st
+
+    def submit(self, op, duty_first, sigs, identifiers, **kw):
+        b, keep, nd, np_ = self._batch(op, duty_first, sigs, identifiers, **kw)
+        t = ctypes.c_uint64()
+        self._check(self._lib.tbg_multi_submit(self._h, ctypes.byref(b), ctypes.byref(t)), "tbg_multi_submit")
+        self._keep[t.value] = (nd, np_)
+        return t.value
+
+    def layout(self, ticket) -> list:
+        out = np.zeros(self.size + 1, dtype=np.uint32)
+        self._check(self._lib.tbg_multi_layout(self._h, ticket, _ptr(out)), "tbg_multi_layout")
+        return out.tolist()
+
+    def collect(self, ticket, block=True):
+        nd, np_ = self._keep[ticket]
+        ps = np.zeros(np_, dtype=np.int32)
+        ds = np.zeros(nd, dtype=np.int32)
+        agg = np.zeros((nd, 96), dtype=np.uint8)
+        rc = self._lib.tbg_multi_collect(self._h, ticket, _ptr(ps), _ptr(ds), _ptr(agg), 1 if block else 0)
+        if rc == E_PENDING:
+            return None
+        del self._keep[ticket]
+        self._check(rc, "tbg_multi_collect")
+        return BatchResult(ps, ds, agg)
+
+    def run(self, op, duty_first, sigs, identifiers, **kw) -> BatchResult:
+        return self.collect(self.submit(op, duty_first, sigs, identifiers, **kw))
+
+
+from .shard import shard_bounds  # noqa: E402,F401  (re-export)
 
 
 _default = {}

@@ -116,6 +116,55 @@ class _PubkeyCache:
 
 _pk_cache = _PubkeyCache()
 
+_PK_ERRORS = {
+    1: "public key is the identity",
+    eng.PS_ERR_FLAGS: "compressed flag must be set / invalid infinity encoding",
+    eng.PS_ERR_FIELD: "invalid bytes - not in field",
+    eng.PS_ERR_CURVE: "point is not on the curve",
+    eng.PS_ERR_SUBGROUP: "point is not in correct subgroup",
+}
+
+
+def key_from_bytes_batch(raws, engine=None):
+    """tblsconv.KeyFromBytes (tblsconv.go:30-37) for many 48-byte keys at once:
+    decoded and validated on the GPU (flags, field, curve, subgroup; the
+    identity is refused as a public key), and made resident.  Per key returns
+    a PublicKey or TblsError("unmarshal pubkey: ...")."""
+    raws = [bytes(r) for r in raws]
+    if not raws:
+        return []
+    e = _engine(engine)
+    for r in raws:
+        if len(r) != 48:
+            raise TblsError("unmarshal pubkey: invalid length")
+    first, st = e.load_pubkeys(b"".join(raws))
+    cache = _pk_cache.ids.setdefault(e.uid, {})
+    out = []
+    for i, (r, s) in enumerate(zip(raws, st.tolist())):
+        if s == 0:
+            cache.setdefault(r, first + i)
+            out.append(PublicKey(r))
+        else:
+            out.append(TblsError("unmarshal pubkey: " + _PK_ERRORS.get(s, str(s))))
+    return out
+
+
+def wire_pubshares(validators, engine=None):
+    """Startup pubshare wiring of app/app.go:334-376 (wireCoreWorkflow):
+    ``validators`` maps a DV public key to its list of 48-byte pubshares (share
+    index = list position + 1).  Every pubshare of the cluster is decoded in
+    ONE GPU batch and stays resident for the verifies that follow; the first
+    bad pubshare, in the reference's loop order, aborts with its
+    KeyFromBytes error (app.go:347-350).  Returns {dv: {share_idx: PublicKey}}."""
+    flat = [(dv, i, bytes(b)) for dv, shares in validators.items() for i, b in enumerate(shares)]
+    keys = key_from_bytes_batch([b for _, _, b in flat], engine)
+    out = {dv: {} for dv in validators}
+    for (dv, i, _), k in zip(flat, keys):
+        if isinstance(k, TblsError):
+            raise k
+        out[dv][i + 1] = k
+    return out
+
 
 def _engine(e):
     return e if e is not None else eng.default_engine()

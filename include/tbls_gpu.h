@@ -70,12 +70,18 @@ typedef enum {
 typedef struct tbg_ctx tbg_ctx;
 typedef uint64_t tbg_ticket;
 
+/* Upper bound of tbg_config.slots: every slot owns one or two HIP streams,
+ * and past ~16 streams per process the HSA runtime runs out of queue
+ * resources (observed on MI355X), so larger values are refused with
+ * TBG_E_INVALID_ARG instead of failing inside HIP. */
+#define TBG_MAX_SLOTS 12
+
 typedef struct {
   int32_t device;         /* HIP device ordinal                           */
   uint32_t max_partials;  /* staging capacity hint (grows on demand)       */
   uint32_t max_duties;
   uint32_t max_msg_bytes;
-  uint32_t slots;         /* in-flight batches, each on its own streams (0 -> 3) */
+  uint32_t slots;         /* in-flight batches, each on its own streams (0 -> 3, <= TBG_MAX_SLOTS) */
   uint32_t verify_mode;   /* TBG_VERIFY_RLC (0, default) or TBG_VERIFY_EACH     */
   uint32_t rlc_group;     /* duties per level-1 RLC group (0 -> 16)              */
   uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests) */
@@ -123,9 +129,15 @@ uint32_t tbg_pubkey_count(const tbg_ctx* ctx);
 int tbg_submit(tbg_ctx* ctx, const tbg_batch* batch, tbg_ticket* ticket);
 
 /* Collect a batch: partial_status [n_partials], duty_status [n_duties],
- * agg96 [n_duties * 96] (any may be NULL).  block = 0 polls. */
+ * agg96 [n_duties * 96] (any may be NULL).  block = 0 polls (TBG_E_PENDING
+ * while running, nothing consumed).  A blocking collect waits WITHOUT the
+ * context lock, so other threads keep submitting / polling meanwhile. */
 int tbg_collect(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status,
                 uint8_t* agg96, int block);
+
+/* Non-consuming readiness check: TBG_OK when finished, TBG_E_PENDING, or an
+ * error code (unknown ticket / device failure). */
+int tbg_poll(tbg_ctx* ctx, tbg_ticket ticket);
 
 /* Convenience: submit + blocking collect. */
 int tbg_run(tbg_ctx* ctx, const tbg_batch* batch, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
@@ -158,6 +170,39 @@ int tbg_sign(tbg_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint8_t* msgs,
  * engine's streams): [decode, hash, combine (RLC sums + group lines),
  * H lines, verify (all check levels), lagrange, aggregate, total]. */
 int tbg_last_timings(const tbg_ctx* ctx, float* ms8);
+
+/* ---- one process, several GPUs (BASELINE config 4) -----------------------
+ * A Charon node is one process: a multi-context owns one tbg_ctx per entry of
+ * devices[] (entries may repeat, e.g. several contexts on one GPU in tests)
+ * and shards every batch across them with no cross-device math.  Duties are
+ * independent, so a batch is cut into contiguous duty ranges
+ * of about equal partial counts, each range is submitted to its context
+ * concurrently (host packing on one thread per context), and tbg_multi_collect
+ * gathers partial_status / duty_status / agg96 straight into the caller's
+ * arrays at the range offsets -- caller order is preserved by construction.
+ * The gathered loops are the per-DV loops of core/parsigex/parsigex.go:101-107
+ * and core/parsigdb/memory.go:96-134 -> core/sigagg/sigagg.go:53-103; the
+ * engine is initialised from the app wiring (app/app.go:321-488).
+ *
+ * Public keys are replicated: tbg_multi_load_pubkeys decodes the table on
+ * every device (1 M DVs x 4 shares is ~0.9 GB of HBM per GPU), so any shard
+ * can reference any id and the ids are the same as for a single context.
+ * cfg->device is ignored (devices[] is used).  Thread-safe. */
+typedef struct tbg_multi tbg_multi;
+int tbg_multi_init(const tbg_config* cfg, const int32_t* devices, uint32_t n_devices, tbg_multi** out);
+void tbg_multi_destroy(tbg_multi* m);
+uint32_t tbg_multi_size(const tbg_multi* m);
+/* The context of shard i (0 <= i < tbg_multi_size), for timings / stats. */
+tbg_ctx* tbg_multi_context(tbg_multi* m, uint32_t i);
+int tbg_multi_load_pubkeys(tbg_multi* m, const uint8_t* pk48, uint32_t count, uint32_t* first_id, int32_t* status);
+int tbg_multi_submit(tbg_multi* m, const tbg_batch* batch, tbg_ticket* ticket);
+/* Same contract as tbg_collect; block = 0 returns TBG_E_PENDING until EVERY
+ * shard has finished (nothing is consumed before that). */
+int tbg_multi_collect(tbg_multi* m, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status,
+                      uint8_t* agg96, int block);
+/* Shard layout of a submitted (not yet collected) ticket: for shard i,
+ * duty range [duty_lo[i], duty_lo[i+1]); arrays of tbg_multi_size()+1. */
+int tbg_multi_layout(tbg_multi* m, tbg_ticket ticket, uint32_t* duty_lo);
 
 #ifdef __cplusplus
 }

@@ -6,13 +6,19 @@ reference's own known-answer vectors (tests/test_oracle_kat.py).  This script
 then freezes inputs and expected outputs for every BASELINE config slice:
 
   cfg1_3of4_single.json     3-of-4, 1 DV, 1 attestation (config 1)
-  cfg2_3of4_sample.json     3-of-4, 8 DVs (sample of config 2 / 4)
-  cfg3_7of10_sample.json    7-of-10, 3 DVs (sample of config 3)
+  cfg2_3of4_sample.json     3-of-4, 64 DVs (sample of config 2 / 4)
+  cfg3_7of10_sample.json    7-of-10, 64 DVs (sample of config 3)
   cfg5_mixed_invalid.json   mixed duties, thresholds {3/4, 5/7, 7/10}, injected
                             wrong-message, wrong-share, random-bytes,
                             non-subgroup, off-curve, bad-flag, identity partials
   aggregate_edges.json      tbls.Aggregate edge cases (identifier 0, duplicate
-                            identifiers, < 2 partials, > t partials, identity)
+                            identifiers, < 2 partials, > t partials, identity,
+                            several D > 1 participant sets, identifier sets whose
+                            integer Lagrange form overflows for some or all
+                            participants)
+  va_id_modes.json          VerifyAndAggregate over clusters with arbitrary
+                            share identifiers (1..255): Lagrange denominators
+                            D > 1, mixed integer / mod-r overflow sets
 
 Seeded with Python's random.Random(seed); run:  python tests/golden/make_golden.py
 """
@@ -238,7 +244,75 @@ def gen_aggregate_edges(rng):
     case("all_four_of_3of4", parts)
     case("subset_124", [parts[0], parts[1], parts[3]])
     case("large_ids", [(200, sigs[0]), (255, sigs[1]), (17, sigs[2]), (99, sigs[3])])
+    # several duties with a Lagrange denominator D > 1 in one batch (the
+    # engine's deferred [1/D] list, k_aggregate_finish)
+    more = [bls.g2_compress(tb.sign(rng.randrange(1, R), msg)) for _ in range(10)]
+    for ids in ([1, 2, 4], [1, 2, 5], [2, 3, 7], [1, 4, 6, 7], [1, 3, 5]):
+        assert lagrange_den(ids) > 1, ids
+        case("den_%s" % "_".join(map(str, ids)), list(zip(ids, more)))
+    # identifier sets whose integer form fits for some participants and not
+    # for others: the encoding must be chosen per duty
+    for tag, ids in (("a", [6, 220, 144, 5, 3, 154]), ("b", [6, 1, 177, 224, 69, 19]),
+                     ("c", [5, 220, 144, 6, 3, 154])):
+        case("mixed_mode_" + tag, list(zip(ids, more)))
+    # every participant overflows the integer form: mod-r coefficients only
+    case("all_modr", list(zip(range(246, 256), more)))
     return out
+
+
+def lagrange_den(ids):
+    """Common denominator of the reduced Lagrange coefficients at 0."""
+    from fractions import Fraction
+    from math import lcm
+    d = 1
+    for i in ids:
+        f = Fraction(1)
+        for j in ids:
+            if j != i:
+                f *= Fraction(j, j - i)
+        d = lcm(d, f.denominator)
+    return d
+
+
+def make_dv_ids(rng, t, ids):
+    """A t-of-len(ids) cluster whose shares sit at arbitrary identifiers."""
+    secret = rng.randrange(1, R)
+    poly = [secret] + [rng.randrange(1, R) for _ in range(t - 1)]
+    shares = {}
+    for x in ids:
+        acc = 0
+        for c in reversed(poly):
+            acc = (acc * x + c) % R
+        shares[x] = acc
+    tss = tb.TSS(pubshares={x: tb.sk_to_pk(s) for x, s in shares.items()}, num_shares=len(ids), threshold=t,
+                 public_key=tb.sk_to_pk(secret))
+    return secret, tss, shares
+
+
+def gen_id_modes(rng):
+    """VerifyAndAggregate with identifier sets that exercise every Lagrange
+    encoding of the engine: D > 1 (deferred [1/D]), mixed integer / mod-r
+    overflow sets and all-mod-r sets; one invalid partial in some duties so
+    the participating set is a strict subset."""
+    recs = []
+    specs = [  # (threshold, identifiers, index of an injected wrong-message partial or None)
+        (3, [1, 2, 3, 4], 2),            # {1,2,4} participate: D = 3
+        (3, [1, 2, 3, 4, 5], 2),         # {1,2,4,5}
+        (2, [1, 2, 4], None),            # D = 3
+        (6, [6, 220, 144, 5, 3, 154], None),
+        (5, [6, 1, 177, 224, 69, 19], 3),
+        (6, [5, 220, 144, 6, 3, 154], None),
+        (10, list(range(246, 256)), None),
+        (4, [200, 255, 17, 99, 1], 0),
+    ]
+    for t, ids, bad in specs:
+        secret, tss, shares = make_dv_ids(rng, t, ids)
+        msg = signing_root(rng, "attestation")
+        parts = honest_partials(shares, msg, ids)
+        if bad is not None:
+            parts[bad] = (parts[bad][0], bls.g2_compress(tb.sign(shares[ids[bad]], msg + b"?")))
+        recs.append(duty_record(rng, secret, tss, shares, msg, parts, "ids_" + "_".join(map(str, ids))))
+    return recs
 
 
 def kat_verify_vectors():
@@ -258,15 +332,84 @@ def kat_verify_vectors():
     return vecs
 
 
+def invalid_pool_file():
+    """tests/golden/invalid_g2.json: encodings the full-size workloads inject
+    (tools/workload.py make_mixed_batch) that need curve arithmetic to find:
+    points on E2 outside G2 (kryptology: subgroup error) and x coordinates
+    with no point on E2 (not-on-curve error), each classified by the oracle."""
+    rng = random.Random(0x1A7A)
+    pools = {"non_subgroup": [], "off_curve": []}
+    for _ in range(24):
+        b = rand_e2_not_in_g2(rng)
+        assert classify(b)[1] == "err_subgroup"
+        pools["non_subgroup"].append(hx(b))
+        b = off_curve_bytes(rng)
+        assert classify(b)[1] == "err_curve"
+        pools["off_curve"].append(hx(b))
+    with open(os.path.join(HERE, "invalid_g2.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py invalid_pool", "seed": "0x1A7A", "pools": pools}, f,
+                  indent=1)
+    # 48-byte G1 public keys for tblsconv.KeyFromBytes (tblsconv.go:30-37):
+    # valid keys and every rejection class, each classified by the oracle
+    g1 = []
+
+    def g1_case(label, b):
+        try:
+            pt = bls.g1_decompress(b)
+            st = "identity" if pt is None else "valid"
+        except bls.DecodeError as e:
+            m = str(e)
+            st = ("err_flags" if ("flag" in m or "infinity" in m) else "err_field" if "field" in m
+                  else "err_curve" if "curve" in m else "err_subgroup")
+        g1.append({"label": label, "pk": hx(b), "expect": st})
+
+    for k in range(4):
+        g1_case("valid", bls.g1_compress(tb.sk_to_pk(rng.randrange(1, R))))
+    good = bls.g1_compress(tb.sk_to_pk(rng.randrange(1, R)))
+    g1_case("bad_flags", bytes([good[0] & 0x7F]) + good[1:])
+    g1_case("identity", bytes([0xC0]) + bytes(47))
+    g1_case("infinity_with_sign", bytes([0xE0]) + bytes(47))
+    g1_case("infinity_with_x", bytes([0xC0]) + good[1:])
+    g1_case("x_ge_p", (bls.P + 5).to_bytes(48, "big")[:0] + bytes([0x80 | ((bls.P + 5) >> 376)]) +
+            (bls.P + 5).to_bytes(48, "big")[1:])
+    g1_case("all_ones", bytes([0x9F]) + bytes([0xFF]) * 47)
+    while len([c for c in g1 if c["label"] == "off_curve"]) < 3:
+        x = rng.randrange(bls.P)
+        y2 = (x * x * x + 4) % bls.P
+        if pow(y2, (bls.P - 1) // 2, bls.P) != 1:
+            b = bytearray(x.to_bytes(48, "big"))
+            b[0] |= 0x80
+            g1_case("off_curve", bytes(b))
+    while len([c for c in g1 if c["label"] == "non_subgroup"]) < 3:
+        x = rng.randrange(bls.P)
+        y2 = (x * x * x + 4) % bls.P
+        if pow(y2, (bls.P - 1) // 2, bls.P) == 1:
+            y = pow(y2, (bls.P + 1) // 4, bls.P)
+            assert not bls.g1_in_subgroup((x, y))
+            g1_case("non_subgroup", bls.g1_compress((x, y)))
+    expected = {"valid": "valid", "bad_flags": "err_flags", "identity": "identity", "infinity_with_sign": "err_flags",
+                "infinity_with_x": "err_flags", "x_ge_p": "err_field", "all_ones": "err_field",
+                "off_curve": "err_curve", "non_subgroup": "err_subgroup"}
+    for c in g1:
+        assert c["expect"] == expected[c["label"]], c
+    with open(os.path.join(HERE, "g1_pubkeys.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py invalid_pool", "seed": "0x1A7A", "vectors": g1}, f,
+                  indent=1)
+
+
 def main():
+    if sys.argv[1:] == ["invalid_pool"]:
+        invalid_pool_file()
+        return
     rng = random.Random(0xC4A2)
     files = {
         "kat_verify.json": kat_verify_vectors(),
         "cfg1_3of4_single.json": gen_cfg(rng, 3, 4, 1),
-        "cfg2_3of4_sample.json": gen_cfg(rng, 3, 4, 8),
-        "cfg3_7of10_sample.json": gen_cfg(rng, 7, 10, 3),
+        "cfg2_3of4_sample.json": gen_cfg(rng, 3, 4, 64),
+        "cfg3_7of10_sample.json": gen_cfg(rng, 7, 10, 64),
         "cfg5_mixed_invalid.json": gen_mixed(rng),
         "aggregate_edges.json": gen_aggregate_edges(rng),
+        "va_id_modes.json": gen_id_modes(rng),
     }
     for name, data in files.items():
         with open(os.path.join(HERE, name), "w") as f:

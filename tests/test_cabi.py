@@ -12,7 +12,7 @@ HEADER = os.path.join(ROOT, "include", "tbls_gpu.h")
 
 def declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\s*\*|uint32_t)\s+(tbg_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\s*\*|uint32_t|tbg_ctx\s*\*)\s*(tbg_\w+)\s*\(", src, re.M)))
 
 
 def lib_path():
@@ -25,7 +25,9 @@ def lib_path():
 def test_header_declares_the_boundary():
     names = declared()
     for must in ["tbg_init", "tbg_destroy", "tbg_load_pubkeys", "tbg_submit", "tbg_collect", "tbg_run",
-                 "tbg_replay", "tbg_replay_multi", "tbg_fetch", "tbg_strerror", "tbg_sign", "tbg_sk_to_pk"]:
+                 "tbg_replay", "tbg_replay_multi", "tbg_fetch", "tbg_strerror", "tbg_sign", "tbg_sk_to_pk",
+                 "tbg_poll", "tbg_multi_init", "tbg_multi_submit", "tbg_multi_collect", "tbg_multi_load_pubkeys",
+                 "tbg_multi_context", "tbg_multi_layout"]:
         assert must in names
 
 
@@ -56,3 +58,5 @@ def test_no_cpu_fallback_without_device():
         pytest.skip("not built")
     with pytest.raises(engine.EngineError):
         engine.Engine(0)
+    with pytest.raises(engine.EngineError):
+        engine.MultiEngine([0, 0])

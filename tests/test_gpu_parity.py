@@ -80,7 +80,7 @@ def _va_batch(engine, vecs):
 
 
 @pytest.mark.parametrize("name", ["cfg1_3of4_single.json", "cfg2_3of4_sample.json", "cfg3_7of10_sample.json",
-                                  "cfg5_mixed_invalid.json"])
+                                  "cfg5_mixed_invalid.json", "va_id_modes.json"])
 def test_verify_and_aggregate_golden(engine, name):
     from charon_amd import engine as eng, tbls
     vecs = load(name)

@@ -221,14 +221,18 @@ def test_aggregate_integer_and_modr_paths_match_golden():
     for v in json.load(open(os.path.join(gold, "aggregate_edges.json")))["vectors"]:
         if v["expect"]["status"] == "ok":
             cases.append(([p["identifier"] for p in v["partials"]], [p["sig"] for p in v["partials"]], v["expect"]["agg"]))
-    for name in ["cfg1_3of4_single.json", "cfg3_7of10_sample.json", "cfg5_mixed_invalid.json"]:
+    for name in ["cfg1_3of4_single.json", "cfg3_7of10_sample.json", "cfg5_mixed_invalid.json", "va_id_modes.json"]:
         for v in json.load(open(os.path.join(gold, name)))["vectors"]:
             if v["expect"]["status"] != "ok":
                 continue
             ps = [p for p, st in zip(v["partials"], v["expect"]["partial_status"]) if st == "valid"]
             cases.append(([p["identifier"] for p in ps], [p["sig"] for p in ps], v["expect"]["agg"]))
     assert len(cases) >= 10
+    # the round-1 advisor's mixed integer / mod-r identifier sets are among them
+    assert any(sorted(ids) == [3, 5, 6, 144, 154, 220] for ids, _, _ in cases)
     for ids, sigs, agg in cases:
+        if len(ids) > 16:
+            continue  # hc_stage_aggregate's fixed arrays
         ob = ctypes.create_string_buffer(96)
         rc = lib().hc_stage_aggregate(bytes(ids), b"".join(bytes.fromhex(s) for s in sigs), len(ids), ob)
         assert rc == 0 and ob.raw.hex() == agg, ids

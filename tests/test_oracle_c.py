@@ -70,7 +70,7 @@ def _va(vecs, threads):
 
 
 @pytest.mark.parametrize("name", ["cfg1_3of4_single.json", "cfg2_3of4_sample.json", "cfg3_7of10_sample.json",
-                                  "cfg5_mixed_invalid.json"])
+                                  "cfg5_mixed_invalid.json", "va_id_modes.json"])
 def test_verify_and_aggregate_golden(name):
     vecs = load(name)
     (ps, ds, agg), duty_first = _va(vecs, threads=4)
@@ -94,3 +94,23 @@ def test_aggregate_golden():
         assert DS_NAMES[int(ds[d])] == v["expect"]["status"], v["label"]
         if v["expect"]["status"] == "ok":
             assert bytes(agg[d]).hex() == v["expect"]["agg"], v["label"]
+
+
+PK_NAMES = {0: "valid", 1: "identity", -1: "err_flags", -2: "err_field", -3: "err_curve", -4: "err_subgroup"}
+
+
+def test_g1_pubkey_rejections():
+    """tblsconv.KeyFromBytes (tblsconv.go:30-37) classes: the C restatement's
+    pubkey table decode gives the oracle's class for every fixture key."""
+    vecs = load("g1_pubkeys.json")
+    table = oc.PubkeyTable(b"".join(bytes.fromhex(v["pk"]) for v in vecs))
+    assert [PK_NAMES[s] for s in table.status.tolist()] == [v["expect"] for v in vecs]
+
+
+def test_invalid_pool_classes():
+    """The committed invalid G2 encodings decode to the class they are named by."""
+    with open(os.path.join(GOLD, "invalid_g2.json")) as f:
+        pools = json.load(f)["pools"]
+    for kind, code in (("non_subgroup", -4), ("off_curve", -3)):
+        for h in pools[kind]:
+            assert oc.g2_decode_status(bytes.fromhex(h)) == code, kind

@@ -20,15 +20,28 @@ import numpy as np
 
 
 def host_cores():
-    n = os.cpu_count() or 1
-    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    return max(1, min(n, cap))
+    """Threads for the CPU baseline: every core this process may use.
+
+    On the GPU pool one GPU's job gets a 16-core share of a 256-core machine
+    (the harness sets OMP_NUM_THREADS=16 there; os.cpu_count() and the
+    affinity mask still report the whole machine).  The share is the host
+    a one-GPU Charon node would have, so that is what is timed; the machine
+    count and the per-core rate are reported beside it so the rate can be
+    scaled.  Elsewhere (no OMP_NUM_THREADS) every core in the affinity mask."""
+    machine = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = machine
+    share = os.environ.get("OMP_NUM_THREADS")
+    n = min(avail, int(share)) if share and share.isdigit() and int(share) > 0 else avail
+    return max(1, n), machine
 
 
 def run_cpu_baseline(batch, seconds: float = 15.0, chunk: int = 512):
     from oracle import c as oc
     oc.build()
-    cores = host_cores()
+    cores, machine = host_cores()
     n = batch.n
     table = oc.PubkeyTable(np.asarray(batch.pubshares, dtype=np.uint8))  # startup decode, untimed
     first_id = int(batch.pubkey_ids[0])
@@ -51,6 +64,8 @@ def run_cpu_baseline(batch, seconds: float = 15.0, chunk: int = 512):
         d0 = d1
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 3), "unit": "DV-duties/s", "cores": cores, "kind": "port",
+            "per_core": round(done / dt / cores, 3), "machine_cores": machine,
             "sample": f"first {done} DVs of the rank-0 bench batch ({batch.t}-of-{n}); C restatement of the "
-                      f"reference per-item schedule (oracle/c), {cores} threads, {dt:.1f}s; not the Go reference",
+                      f"reference per-item schedule (oracle/c), {cores} threads = this job's core share "
+                      f"(OMP_NUM_THREADS; the machine has {machine}), {dt:.1f}s; not the Go reference",
             "mismatches": mismatches}
