@@ -79,7 +79,9 @@ template <class F> TBG_HD Jac<F> jac_dbl_in(const Jac<F>& p) {
 #endif
 
 // add-2007-bl with the exceptional cases handled (P == Q, P == -Q, infinity).
-template <class F> TBG_HD Jac<F> jac_add_in(const Jac<F>& p, const Jac<F>& q) {
+// INLDBL = true doubles inline in the P == Q case (no out-of-line call in the
+// caller's loop; see TBG_ADD_DBL below).
+template <class F, bool INLDBL = false> TBG_HD Jac<F> jac_add_in(const Jac<F>& p, const Jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = f_sqr(p.Z);
@@ -91,7 +93,7 @@ template <class F> TBG_HD Jac<F> jac_add_in(const Jac<F>& p, const Jac<F>& q) {
   F H = f_reduce(f_sub(U2, U1));
   F Rr = f_reduce(f_sub(S2, S1));
   if (f_is_zero(H)) {
-    if (f_is_zero(Rr)) return jac_dbl(p);
+    if (f_is_zero(Rr)) return INLDBL ? jac_dbl_in(p) : jac_dbl(p);
     return jac_inf<F>();
   }
   F H2 = f_add(H, H);
@@ -184,6 +186,17 @@ template <class F> TBG_HD Jac<F> jac_mul_xabs_in(const Jac<F>& p) {
   for (int i = 62; i >= 0; --i) {
     acc = jac_dbl_in(acc);
     if ((X_ABS >> i) & 1) acc = jac_add_in(acc, p);
+  }
+  return acc;
+}
+
+// Same, with the P == Q case of the additions doubled inline too (no
+// out-of-line call anywhere in the loop; the lane-pair kernels need that).
+template <class F> TBG_HD Jac<F> jac_mul_xabs_in2(const Jac<F>& p) {
+  Jac<F> acc = p;
+  for (int i = 62; i >= 0; --i) {
+    acc = jac_dbl_in(acc);
+    if ((X_ABS >> i) & 1) acc = jac_add_in<F, true>(acc, p);
   }
   return acc;
 }
@@ -283,8 +296,10 @@ enum DecodeStatus : int32_t {
 };
 
 // 96-byte ZCash compressed G2 -> affine (Montgomery).  INL = true runs the
-// subgroup check's doublings inline (kernel callers).
-template <bool INL>
+// subgroup check's doublings inline (kernel callers); SUBGROUP = false leaves
+// the subgroup check to the caller (k_decode_sigs hands it to the lane-pair
+// kernel k_subgroup_sigs, bls_pair.h).
+template <bool INL, bool SUBGROUP = true>
 TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out) {
   uint32_t c_flag = (b[0] >> 7) & 1, i_flag = (b[0] >> 6) & 1, s_flag = (b[0] >> 5) & 1;
   if (!c_flag) return DEC_ERR_FLAGS;
@@ -307,7 +322,7 @@ TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out) {
   if ((uint32_t)fp2_lex_largest(y) != s_flag) y = fp2_reduce(fp2_neg(y));
   out.x = x;
   out.y = y;
-  if (!(INL ? g2_in_subgroup_aff_in(out) : g2_in_subgroup(jac_from_aff(out)))) return DEC_ERR_SUBGROUP;
+  if (SUBGROUP && !(INL ? g2_in_subgroup_aff_in(out) : g2_in_subgroup(jac_from_aff(out)))) return DEC_ERR_SUBGROUP;
   return DEC_OK;
 }
 TBG_NI int32_t g2_decompress(const uint8_t* b, G2A& out) { return g2_decompress_t<false>(b, out); }

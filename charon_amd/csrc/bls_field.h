@@ -194,6 +194,18 @@ TBG_HD Fp fp_canon(const Fp& a) { return fp_csub_p(fp_reduce(a)); }
 static_assert(TBG_ACC_AB == 1 || TBG_ACC_AB == 2 || TBG_ACC_AB == 4, "TBG_ACC_AB");
 static_assert(TBG_ACC_MP == 1 || TBG_ACC_MP == 2, "TBG_ACC_MP");
 
+// TBG_SCHED_FENCE=1 (set per translation unit before the includes): a
+// scheduling barrier around every Montgomery product, so the machine
+// scheduler does not interleave independent products for ILP -- each product
+// already has six independent accumulator chains, and interleaving two of
+// them is what pushes the point kernels past 256 VGPRs (two waves per SIMD,
+// which hide latency better than the interleaving does).
+#if defined(__HIP_DEVICE_COMPILE__) && defined(TBG_SCHED_FENCE) && TBG_SCHED_FENCE
+#define TBG_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define TBG_FENCE() ((void)0)
+#endif
+
 template <int N>
 TBG_HD uint64_t acc_total(const uint64_t (&s)[N]) {
   if constexpr (N == 4) return (s[0] + s[1]) + (s[2] + s[3]);
@@ -204,6 +216,7 @@ TBG_HD uint64_t acc_total(const uint64_t (&s)[N]) {
 template <int K>
 TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
   TBG_COUNT(196 * (K + 1));
+  TBG_FENCE();
   uint32_t m[NL];
   Fp r;
   uint64_t acc = 0;
@@ -235,6 +248,7 @@ TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
     acc = sum >> 28;
   }
   r.l[NL - 1] = (uint32_t)acc;
+  TBG_FENCE();
   return r;
 }
 
@@ -258,6 +272,7 @@ TBG_HD Fp fp_mul2(const Fp& a, const Fp& b, const Fp& c, const Fp& d) {
 TBG_HD Fp fp_sqr(const Fp& a) {
   TBG_BOUND(fp_ratio_p(a) * fp_ratio_p(a) < 2048.0, "fp_sqr bound");
   TBG_COUNT(301);
+  TBG_FENCE();
   uint32_t a2[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) a2[i] = a.l[i] << 1;
@@ -289,6 +304,7 @@ TBG_HD Fp fp_sqr(const Fp& a) {
     acc = sum >> 28;
   }
   r.l[NL - 1] = (uint32_t)acc;
+  TBG_FENCE();
   return r;
 }
 

@@ -136,4 +136,52 @@ TBG_HD void rlc_mul_both(const G2A& s, const G1A& pk, const G1A& xpk, const uint
   }
 }
 
+// ---------------------------------------------------------------------------
+// Inversion-free form (the split kernels k_rlc_g1 / k_rlc_g2_pair): the pair
+// table A+- = q0 +- q1 stays Jacobian (one mixed addition each) and the 31
+// table additions are full Jacobian additions.  Against the affine table this
+// trades the field inversion (~480 Fp products, which the two lanes of a
+// pair would both run) for 31 x (4M + 1S) extra products that the pair
+// splits -- and it keeps no inversion on the lane at all.
+template <class F>
+TBG_HD Jac<F> rlc_entry_j(const Jac<F>& ap, const Jac<F>& am, uint32_t b0, uint32_t b1, bool endo, const Fp& c) {
+  const bool same = b0 == b1;
+  const bool negy = (b0 != 0) == endo;
+  Jac<F> e;
+  e.X = same ? ap.X : am.X;
+  e.Z = same ? ap.Z : am.Z;
+  const F y = same ? ap.Y : am.Y;
+  const F ny = f_reduce(f_neg(y));
+  e.Y = negy ? ny : y;
+  if (endo) e.X = rlc_mul_c(e.X, c);  // (x, y) -> (c x, -y): X scales like x
+  return e;
+}
+
+template <class F>
+TBG_HD void rlc_pair_jac(const Aff<F>& q0, const Aff<F>& q1, Jac<F>& ap, Jac<F>& am) {
+  const Jac<F> j0 = jac_from_aff(q0);
+  ap = jac_add_aff_in(j0, q1);
+  am = jac_add_aff_in(j0, Aff<F>{q1.x, f_reduce(f_neg(q1.y))});
+}
+
+template <class F>
+TBG_HD Jac<F> rlc_mul_table_j(const Jac<F>& ap, const Jac<F>& am, const Fp& c, const uint32_t (&u)[4]) {
+  Jac<F> acc = rlc_entry_j(ap, am, (u[0] >> 15) & 1, (u[1] >> 15) & 1, false, c);
+  acc = jac_add_in<F, true>(acc, rlc_entry_j(ap, am, (u[2] >> 15) & 1, (u[3] >> 15) & 1, true, c));
+#pragma unroll 1
+  for (int bit = 14; bit >= 0; --bit) {
+    acc = jac_dbl_in(acc);
+    acc = jac_add_in<F, true>(acc, rlc_entry_j(ap, am, (u[0] >> bit) & 1, (u[1] >> bit) & 1, false, c));
+    acc = jac_add_in<F, true>(acc, rlc_entry_j(ap, am, (u[2] >> bit) & 1, (u[3] >> bit) & 1, true, c));
+  }
+  return acc;
+}
+
+// [r] pk on G1, inversion-free: pairs (pk, [x]pk) and -phi of the same table.
+TBG_HD G1J rlc_mul_g1_j(const G1A& pk, const G1A& xpk, const uint32_t (&u)[4]) {
+  G1J ap, am;
+  rlc_pair_jac(pk, xpk, ap, am);
+  return rlc_mul_table_j(ap, am, fp_from_const(G1_BETA), u);
+}
+
 }  // namespace tbg

@@ -3,8 +3,12 @@
 // The P == Q case of the mixed addition doubles inline (bls_curve.h): no
 // out-of-line call inside the kernels' point loops.
 #define TBG_ADD_DBL_INLINE 1
+#ifndef TBG_SCHED_FENCE
+#define TBG_SCHED_FENCE 1  // products in program order: fits the pair kernel in 256 VGPRs (bls_field.h)
+#endif
 #include "tbls_launch.h"
 #include "bls_curve.h"
+#include "bls_pair.h"
 
 namespace tbg {
 
@@ -30,13 +34,19 @@ __global__ void TBG_LAUNCH k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A
   status[i] = st;
 }
 
-__global__ void TBG_LAUNCH k_decode_sigs(DevBatch B) {
+// Decode in two kernels so each runs at the occupancy its own register
+// footprint allows (one kernel would take the maximum of both):
+//   k_decode_sigs    one lane per signature: flags, field, Fp2 square root
+//                    (Fp exponentiations: small state, several waves per SIMD);
+//   k_subgroup_sigs  one lane PAIR per decoded signature: psi(a) == [x] a with
+//                    the Fp2 coordinates split over the pair (bls_pair.h).
+__global__ void TBG_LAUNCH_N(TBG_DECODE_WAVES) k_decode_sigs(DevBatch B) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B.n_partials) return;
   uint8_t b[96];
   for (int j = 0; j < 96; ++j) b[j] = B.sigs[96ull * i + j];
   G2A a;
-  int32_t st = g2_decompress_t<true>(b, a);
+  int32_t st = g2_decompress_t<true, false>(b, a);
   if (st == DEC_IDENTITY) st = TBG_PS_ERR_IDENTITY;
   if (st != DEC_OK) {
     a.x = fp2_zero();
@@ -46,11 +56,32 @@ __global__ void TBG_LAUNCH k_decode_sigs(DevBatch B) {
   B.partial_status[i] = (st == DEC_OK) ? TBG_PS_NOT_VERIFIED : st;
 }
 
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_subgroup_sigs(DevBatch B) {
+  const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
+  if (i >= B.n_partials) return;
+  if (B.partial_status[i] != TBG_PS_NOT_VERIFIED) return;
+  const Aff<Fp2x> a = px_load(B.sig_aff[i]);
+  bool exc = false;
+  bool ok = g2_in_subgroup_aff_g(a, exc);
+  if (exc) {
+    // an addition of [|x|] a met its doubling case (only for points of tiny
+    // order, i.e. crafted signatures): decide on the single-lane reference
+    // path, out of line so the loop above keeps its registers
+    ok = g2_in_subgroup(jac_from_aff(B.sig_aff[i]));
+  }
+  if (!ok && pair_par() == 0) {
+    B.partial_status[i] = TBG_PS_ERR_SUBGROUP;
+    B.sig_aff[i] = G2A{fp2_zero(), fp2_zero()};
+  }
+}
+
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st) {
   if (n) TBG_KLAUNCH(k_decode_pubkeys, grid_for(n), dim3(kBlock), st, pk48, n, out, out_x, status);
 }
 void launch_decode_sigs(const DevBatch& B, hipStream_t st) {
-  if (B.n_partials) TBG_KLAUNCH(k_decode_sigs, grid_for(B.n_partials), dim3(kBlock), st, B);
+  if (!B.n_partials) return;
+  TBG_KLAUNCH(k_decode_sigs, grid_for(B.n_partials), dim3(kBlock), st, B);
+  TBG_KLAUNCH(k_subgroup_sigs, grid_for(2 * B.n_partials), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

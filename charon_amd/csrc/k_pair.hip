@@ -1,0 +1,114 @@
+// Level-0 RLC products [r_i] s_i (G2) and [r_i] pk_i (G1), one lane per
+// partial for the Fp-level work and one lane PAIR for the G2 point work
+// (bls_pair.h: halves the G2 state per lane so the kernel fits two waves per
+// SIMD, which on gfx950 issue the multiply-adds ~1.7x faster than one).
+//
+//   phase 1, lane L owns partial L: one field inversion shared by both pair
+//            tables (Montgomery's trick, as the fused single-lane kernel did),
+//            then the whole G1 product on the lane;
+//   phase 2, lanes (2k, 2k+1) run the G2 table and its 15 doublings + 31
+//            additions for partial 2k, then for 2k+1, with the Fp2
+//            coordinates split over the pair and the owner's inverse and
+//            digits handed over by DPP.
+//
+// Measured and rejected: separate G1 / pair-G2 kernels with inversion-free
+// Jacobian tables (bls_rlc.h *_j) -- 446 spilled VGPRs in the pair kernel,
+// 3.19 ms against 2.85 ms for the fused single-lane kernel.
+#define TBG_ADD_DBL_INLINE 1
+#ifndef TBG_SCHED_FENCE
+#define TBG_SCHED_FENCE 1  // products in program order: fits the pair kernel in 256 VGPRs (bls_field.h)
+#endif
+#include "tbls_launch.h"
+#include "bls_rlc.h"
+#include "bls_pair.h"
+
+namespace tbg {
+
+__device__ __forceinline__ bool rlc_usable_pk(const DevBatch& B, uint32_t i, const int32_t* pk_status, uint32_t n_pk) {
+  int32_t st = B.partial_status[i];
+  if (st != TBG_PS_NOT_VERIFIED && st != TBG_PS_ERR_PUBKEY) return false;
+  uint32_t pid = B.pubkey_ids[i];
+  return pid < n_pk && pk_status[pid] == DEC_OK;
+}
+
+// Only the first usable candidate of the whole level-1 GROUP takes r = 1 (a
+// fixed coefficient per duty would let two invalid partials of different
+// duties in one group cancel; k_rlc.hip).  Both kernels decide it the same way
+// whichever of them has already marked bad-key partials ERR_PUBKEY.
+__device__ __forceinline__ bool rlc_group_lead(const DevBatch& B, uint32_t i, const int32_t* pk_status, uint32_t n_pk) {
+  const uint32_t d = B.partial_duty[i];
+  const uint32_t d0 = (d / B.rlc_group) * B.rlc_group;
+  for (uint32_t j = B.duty_first[d0]; j < i; ++j)
+    if (rlc_usable_pk(B, j, pk_status, n_pk)) return false;
+  return true;
+}
+
+// The pair-owner's Fp2 value (owner = the lane of parity j) in pair form:
+// every lane sends the component its partner needs, the owner keeps its own.
+__device__ __forceinline__ Fp2x px_from_owner(const Fp2& own, uint32_t j) {
+  const uint32_t par = pair_par();
+  const Fp recv = pair_xch(par ? own.c0 : own.c1);  // the partner's value, component par
+  return {par == j ? (par ? own.c1 : own.c0) : recv};
+}
+__device__ __forceinline__ uint32_t u32_from_owner(uint32_t own, uint32_t j) {
+  const uint32_t recv = pair_u32(own);
+  return pair_par() == j ? own : recv;
+}
+
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_rlc_partial2(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
+                                                             const int32_t* pk_status, uint32_t n_pk) {
+  // No early return: both lanes of every pair must reach the DPP exchanges.
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool active = i < B.n_partials && B.partial_status[i] == TBG_PS_NOT_VERIFIED;
+  uint32_t pid = 0;
+  if (active) {
+    pid = B.pubkey_ids[i];
+    if (pid >= n_pk || pk_status[pid] != DEC_OK) {
+      B.partial_status[i] = TBG_PS_ERR_PUBKEY;
+      active = false;
+    }
+  }
+  const bool lead = active && rlc_group_lead(B, i, pk_status, n_pk);
+  const bool work = active && !lead;
+  uint32_t a[4] = {0, 0, 0, 0};
+  Fp2 inv2 = fp2_zero();
+  if (lead) {
+    B.part_s[i] = jac_from_aff(B.sig_aff[i]);
+    B.part_p[i] = jac_from_aff(pk_aff[pid]);
+  } else if (work) {
+    rlc_digits(rlc_scalar(B.rlc_seed, i), a);
+    const G2A s = B.sig_aff[i];
+    const G1A p0 = pk_aff[pid], x0 = xpk_aff[pid];
+    // 1 / (psi(s).x - s.x) and 1 / ([x]pk.x - pk.x) from ONE inversion
+    const Fp2 dx2 = fp2_reduce(fp2_sub(fp2_mul(fp2_conj(s.x), fp2_from_const(PSI_X)), s.x));
+    const Fp dx1 = fp_reduce(fp_sub(x0.x, p0.x));
+    const Fp n2 = fp_mul2(dx2.c0, dx2.c0, dx2.c1, dx2.c1);
+    const Fp t = fp_inv(fp_mul(n2, dx1));
+    const Fp in2 = fp_mul(t, dx1);
+    inv2 = Fp2{fp_mul(dx2.c0, in2), fp_mul(fp_neg(dx2.c1), in2)};
+    G1A ap, am;
+    rlc_pair_from_inv(p0, x0, fp_mul(t, n2), ap, am);
+    B.part_p[i] = rlc_mul_table(ap, am, fp_from_const(G1_BETA), a);
+  }
+  for (uint32_t j = 0; j < 2; ++j) {
+    if (!u32_from_owner(work ? 1u : 0u, j)) continue;  // pair-uniform
+    const uint32_t owner = (i & ~1u) | j;
+    const Fp2x ix = px_from_owner(inv2, j);
+    uint32_t u[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = u32_from_owner(a[k], j);
+    const Aff<Fp2x> s = px_load(B.sig_aff[owner]);
+    const Aff<Fp2x> ps{f_mulc(f_conj(s.x), PSI_X), f_mulc(f_conj(s.y), PSI_Y)};  // psi(s) = [x] s
+    Aff<Fp2x> ap, am;
+    rlc_pair_from_inv(s, ps, ix, ap, am);
+    px_store(B.part_s[owner], rlc_mul_table(ap, am, fp_from_const(PSI2_X), u));
+  }
+}
+
+void launch_rlc_partials(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status,
+                         uint32_t n_pk, hipStream_t st) {
+  if (!B.n_partials) return;
+  TBG_KLAUNCH(k_rlc_partial2, grid_for(B.n_partials), dim3(kBlock), st, B, pk_aff, xpk_aff, pk_status, n_pk);
+}
+
+}  // namespace tbg

@@ -46,43 +46,7 @@ __device__ __forceinline__ bool rlc_candidate(const DevBatch& B, uint32_t i) {
 }
 
 // ------------------------------------------------------------------ level 0
-// One thread per partial: [r_i] s_i and [r_i] pk_i by the base-x digit
-// method of bls_rlc.h (four-point, 16-bit Straus products).
-__global__ void TBG_LAUNCH k_rlc_partial(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
-                                                    const int32_t* pk_status, uint32_t n_pk) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B.n_partials) return;
-  if (!rlc_candidate(B, i)) return;
-  uint32_t pid = B.pubkey_ids[i];
-  if (pid >= n_pk || pk_status[pid] != DEC_OK) {
-    B.partial_status[i] = TBG_PS_ERR_PUBKEY;
-    return;
-  }
-  // Only the first candidate of the whole level-1 GROUP takes r = 1.  (A
-  // fixed coefficient per duty would let two invalid partials of different
-  // duties in one group cancel: s_a = sig_a + D, s_b = sig_b - D.)  The duty
-  // sums S_d, P_d then carry random coefficients on all but at most one
-  // partial, which keeps the level-2 (per-duty) equations sound as well.
-  const uint32_t d = B.partial_duty[i];
-  const uint32_t d0 = (d / B.rlc_group) * B.rlc_group;
-  bool lead = true;
-  for (uint32_t j = B.duty_first[d0]; j < i && lead; ++j)
-    if (rlc_usable(B, j, pk_status, n_pk)) lead = false;
-  const G2A s0 = B.sig_aff[i];
-  const G1A p0 = pk_aff[pid];
-  if (lead) {
-    B.part_s[i] = jac_from_aff(s0);
-    B.part_p[i] = jac_from_aff(p0);
-    return;
-  }
-  uint32_t a[4];
-  rlc_digits(rlc_scalar(B.rlc_seed, i), a);
-  G2J S;
-  G1J P;
-  rlc_mul_both(s0, p0, xpk_aff[pid], a, S, P);
-  B.part_s[i] = S;
-  B.part_p[i] = P;
-}
+// [r_i] s_i and [r_i] pk_i: k_rlc_g2_pair / k_rlc_g1 (k_pair.hip).
 
 // One thread per duty: P_d = sum r_i pk_i (affine) and S_d = sum r_i s_i.
 __global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B) {
@@ -362,8 +326,7 @@ void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff
     if (B.n_partials) TBG_KLAUNCH(k_list_all_partials, grid_for(B.n_partials), dim3(kBlock), st, B, pk_status, n_pk);
     return;
   }
-  if (B.n_partials)
-    TBG_KLAUNCH(k_rlc_partial, grid_for(B.n_partials), dim3(kBlock), st, B, pk_aff, xpk_aff, pk_status, n_pk);
+  launch_rlc_partials(B, pk_aff, xpk_aff, pk_status, n_pk, st);
   TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B);
   uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
   TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);

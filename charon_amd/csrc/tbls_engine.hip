@@ -370,6 +370,7 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   size_t w_sig_aff = sec(sizeof(G2A) * (size_t)np);
   size_t w_h_aff = sec(sizeof(G2A) * (size_t)nm);
   size_t w_h_st = sec(4ull * nm);
+  size_t w_h_jac = sec(sizeof(G2J) * (size_t)nm);
   size_t w_lam = sec(32ull * np);
   size_t w_sl = sec(verify ? 4ull * LINES_WORDS * np : 0);
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
@@ -441,6 +442,7 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   B.sig_aff = (G2A*)(dw + w_sig_aff);
   B.h_aff = (G2A*)(dw + w_h_aff);
   B.h_status = (int32_t*)(dw + w_h_st);
+  B.h_jac = (G2J*)(dw + w_h_jac);
   B.lam = (uint32_t*)(dw + w_lam);
   B.sig_lines = (uint32_t*)(dw + w_sl);
   B.h_lines = (uint32_t*)(dw + w_hl);
@@ -698,7 +700,8 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
   HIP_TRY(hipSetDevice(c->device));
   size_t mb = msg_off[n_msgs];
   size_t need = align_up(32ull * n, 16) + align_up(mb + 1, 16) + align_up(4ull * (n_msgs + 1), 16) + align_up(4ull * n, 16) +
-                align_up(sizeof(G2A) * (size_t)n_msgs, 16) + align_up(4ull * n_msgs, 16) + align_up(96ull * n, 16);
+                align_up(sizeof(G2A) * (size_t)n_msgs, 16) + align_up(4ull * n_msgs, 16) + align_up(96ull * n, 16) +
+                align_up(sizeof(G2J) * (size_t)n_msgs, 16);
   uint8_t* base = nullptr;
   if (hipMalloc(&base, need) != hipSuccess) return TBG_E_OOM;
   size_t o = 0;
@@ -710,6 +713,7 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
   G2A* d_h = (G2A*)sec(sizeof(G2A) * (size_t)n_msgs);
   int32_t* d_hs = (int32_t*)sec(4ull * n_msgs);
   uint8_t* d_sig = sec(96ull * n);
+  G2J* d_hj = (G2J*)sec(sizeof(G2J) * (size_t)n_msgs);
   int rc = TBG_OK;
   hipStream_t st = c->stream;
   if (hipMemcpyAsync(d_sk, sk32, 32ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -725,6 +729,7 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
     B.msg_off = d_off;
     B.h_aff = d_h;
     B.h_status = d_hs;
+    B.h_jac = d_hj;
     launch_hash_msgs(B, st);
     launch_sign(d_sk, d_im, n, d_h, d_hs, d_sig, st);
     if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;

@@ -18,6 +18,16 @@ constexpr int kBlock = 64;
 #define TBG_MIN_WAVES 1
 #endif
 #define TBG_LAUNCH __launch_bounds__(64, TBG_MIN_WAVES)
+// Kernels split by phase ask for the occupancy their footprint allows: at
+// least two waves per SIMD (<= 256 VGPRs), because a lone wave issues the
+// multiply-adds at ~58 % of the two-wave rate (profiles/r02/valu_rates.txt).
+#ifndef TBG_PAIR_WAVES
+#define TBG_PAIR_WAVES 2    // lane-pair G2 kernels (bls_pair.h)
+#endif
+#ifndef TBG_DECODE_WAVES
+#define TBG_DECODE_WAVES 2  // k_decode_sigs (square roots only)
+#endif
+#define TBG_LAUNCH_N(w) __launch_bounds__(64, w)
 inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
 // Device-side layout of one batch (all pointers into device memory).
@@ -36,6 +46,7 @@ struct DevBatch {
   G2A* sig_aff;
   G2A* h_aff;
   int32_t* h_status;
+  G2J* h_jac;          // [n_msgs] H(m) before affine conversion (k_hash_map / _clear / _affine)
   uint32_t* lam;       // [n_partials][8] scalar words
   uint32_t* sig_lines;  // [n_partials][LINES_WORDS] Miller lines of listed signatures (-g1 folded in)
   uint32_t* h_lines;    // [n_msgs][LINES_WORDS] Miller lines of each H(m) (G1 factor left out)
@@ -87,10 +98,13 @@ void debug_after_launch(const char* kernel, hipStream_t st);
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st);
 void launch_decode_sigs(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);
+void launch_hash_clear(const DevBatch& B, hipStream_t st);
 void launch_h_lines(const DevBatch& B, hipStream_t st);
 void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
                         hipStream_t st);
 void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
+void launch_rlc_partials(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status,
+                         uint32_t n_pk, hipStream_t st);
 void launch_lagrange(const DevBatch& B, hipStream_t st);
 void launch_aggregate(const DevBatch& B, hipStream_t st);
 void launch_aggregate_finish(const DevBatch& B, hipStream_t st);

@@ -462,3 +462,69 @@ void hc_stage_group_final(int nch) {
   f = qe::final_exp(qe::conj(f));
 }
 }
+
+#include "../../charon_amd/csrc/bls_pair.h"
+// Lane-pair Fp2 (bls_pair.h), host-emulated: the two lanes' pieces side by side.
+extern "C" {
+// out: mul(a, b), sqr(a), inv(a), conj(a), mul_xi(a), a * PSI_X -- 6 x 96 bytes (c0 || c1 canonical BE)
+static void f2_out_pp(const Fp2p& x, uint8_t* out) {
+  fp_limbs_to_be48(fp_from_mont(x.c0), out);
+  fp_limbs_to_be48(fp_from_mont(x.c1), out + 48);
+}
+static Fp2p f2_in_pp(const uint8_t* in) {
+  bool lt;
+  return {fp_to_mont(fp_limbs_from_be48(in, &lt)), fp_to_mont(fp_limbs_from_be48(in + 48, &lt))};
+}
+void hc_pair_ops(const uint8_t* a96, const uint8_t* b96, uint8_t* out) {
+  Fp2p a = f2_in_pp(a96), b = f2_in_pp(b96);
+  f2_out_pp(f_mul(a, b), out);
+  f2_out_pp(f_sqr(a), out + 96);
+  f2_out_pp(f_inv(a), out + 192);
+  f2_out_pp(f_reduce(pp_conj(a)), out + 288);
+  f2_out_pp(f_reduce(pp_mul_xi(a)), out + 384);
+  f2_out_pp(pp_mul_const(a, PSI_X), out + 480);
+}
+// k_decode_sigs + k_subgroup_sigs: decode without the subgroup check, then the
+// pair-emulated check; returns a DecodeStatus like g2_decompress.
+int hc_pair_decode_sig(const uint8_t* sig96) {
+  G2A a;
+  int st = g2_decompress_t<true, false>(sig96, a);
+  if (st != DEC_OK) return st;
+  Aff<Fp2p> p{pp_from(a.x), pp_from(a.y)};
+  bool exc = false;
+  bool ok = g2_in_subgroup_aff_g(p, exc);
+  if (exc) ok = g2_in_subgroup(jac_from_aff(a));
+  return ok ? DEC_OK : DEC_ERR_SUBGROUP;
+}
+}
+
+// Inversion-free RLC products (bls_rlc.h *_j, the split kernels k_rlc_g1 /
+// k_rlc_g2_pair): G1, single-lane G2 and the pair-emulated G2, each against
+// the plain 255-bit double-and-add [r mod order] P.  Bits 1 | 2 | 4.
+extern "C" int hc_rlc_check_j(const uint8_t* sig96, const uint8_t* pk48, uint64_t r64, const uint32_t* r_words) {
+  G2A s;
+  G1A pk;
+  if (g2_decompress(sig96, s) != DEC_OK || g1_decompress(pk48, pk) != DEC_OK) return -1;
+  uint32_t a[4];
+  rlc_digits(r64, a);
+  G2J S_ref = jac_mul_words(jac_from_aff(s), r_words, 255);
+  G1J P_ref = jac_mul_words(jac_from_aff(pk), r_words, 255);
+  int out = 0;
+  if (jac_eq(rlc_mul_g1_j(pk, hc_xpk(pk), a), P_ref)) out |= 1;
+  {
+    G2A ps = g2_psi_aff(s);
+    G2J ap, am;
+    rlc_pair_jac(s, ps, ap, am);
+    if (jac_eq(rlc_mul_table_j(ap, am, fp_from_const(PSI2_X), a), S_ref)) out |= 2;
+  }
+  {
+    Aff<Fp2p> sp{pp_from(s.x), pp_from(s.y)};
+    Aff<Fp2p> psp{f_mulc(f_conj(sp.x), PSI_X), f_mulc(f_conj(sp.y), PSI_Y)};
+    Jac<Fp2p> ap, am;
+    rlc_pair_jac(sp, psp, ap, am);
+    Jac<Fp2p> S = rlc_mul_table_j(ap, am, fp_from_const(PSI2_X), a);
+    G2J Sg{pp_to(S.X), pp_to(S.Y), pp_to(S.Z)};
+    if (jac_eq(Sg, S_ref)) out |= 4;
+  }
+  return out;
+}

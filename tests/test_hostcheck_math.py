@@ -290,6 +290,10 @@ def test_rlc_digit_scalars_match_plain_scalar_multiplication():
         r = sum(a[k] * x ** k for k in range(4)) % bls.R
         words = (ctypes.c_uint32 * 8)(*[(r >> (32 * k)) & 0xFFFFFFFF for k in range(8)])
         assert L.hc_rlc_check(sig, pk, r64, words) == 3
+        # inversion-free Jacobian tables: G1, single-lane G2, lane-pair G2 (emulated)
+        L.hc_rlc_check_j.restype = ctypes.c_int
+        L.hc_rlc_check_j.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+        assert L.hc_rlc_check_j(sig, pk, r64, words) == 7
 
 
 def test_rlc_digit_scalars_are_distinct_mod_r():
@@ -298,3 +302,42 @@ def test_rlc_digit_scalars_are_distinct_mod_r():
     x = bls.X_ABS
     # signed digits a_k = 2 u_k - (2^16 - 1): differences of two are < 2^17
     assert (1 << 17) < x and (1 << 17) * x ** 3 < bls.R
+
+
+def test_lane_pair_fp2_matches_tower():
+    """bls_pair.h: Fp2 split over two lanes (host-emulated pair) equals the
+    oracle's Fp2 arithmetic for every operation the pair kernels use."""
+    import ctypes
+    L = lib()
+    psi_x = bls.f2_inv(bls.f2_pow((1, 1), (P - 1) // 3))  # tools/gen_constants.py PSI_X
+    for _ in range(6):
+        a = (rng.randrange(P), rng.randrange(P))
+        b = (rng.randrange(P), rng.randrange(P))
+        out = ctypes.create_string_buffer(6 * 96)
+        enc = lambda x: x[0].to_bytes(48, "big") + x[1].to_bytes(48, "big")  # noqa: E731
+        L.hc_pair_ops(enc(a), enc(b), out)
+        got = [(int.from_bytes(out.raw[96 * k:96 * k + 48], "big") % P, int.from_bytes(out.raw[96 * k + 48:96 * k + 96], "big") % P)
+               for k in range(6)]
+        assert got[0] == bls.f2_mul(a, b)
+        assert got[1] == bls.f2_sqr(a)
+        assert got[2] == bls.f2_inv(a)
+        assert got[3] == bls.f2_conj(a)
+        assert got[4] == bls.f2_mul_xi(a)
+        assert got[5] == bls.f2_mul(a, psi_x)
+
+
+def test_lane_pair_subgroup_check_matches_decode():
+    """k_decode_sigs + k_subgroup_sigs (pair-emulated) classify like the
+    single-lane decode: valid signatures, non-subgroup points, off-curve."""
+    import json
+    import os
+    L = lib()
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    pools = json.load(open(os.path.join(gold, "invalid_g2.json")))["pools"]
+    for h in pools["non_subgroup"][:4]:
+        assert L.hc_pair_decode_sig(bytes.fromhex(h)) == -4
+    for h in pools["off_curve"][:2]:
+        assert L.hc_pair_decode_sig(bytes.fromhex(h)) == -3
+    for v in json.load(open(os.path.join(gold, "cfg1_3of4_single.json")))["vectors"]:
+        for p in v["partials"]:
+            assert L.hc_pair_decode_sig(bytes.fromhex(p["sig"])) == 0
