@@ -123,7 +123,7 @@ def stage_mads(wm, args):
     """Algorithmic u32 mul-adds per launch of each stage for one clean batch
     (work model of tools/count_work.py: RLC group G = 16, chunk C = 4)."""
     m = wm["mads"]
-    nd, n = args.dvs, args.n
+    nd, n = args.dvs * max(1, args.merge), args.n  # one launch covers `merge` batches
     np_ = nd * n
     G = wm.get("rlc_schedule", {}).get("group", 16)
     ng = (nd + G - 1) // G
@@ -240,7 +240,9 @@ def main():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--inflight", type=int, default=8, help="resident batches replayed round-robin (engine slots)")
+    ap.add_argument("--inflight", type=int, default=8, help="engine slots replayed round-robin (launches in flight)")
+    ap.add_argument("--merge", type=int, default=1,
+                    help="10k-DV batches per slot, submitted together as one device batch (tbg_submit_group)")
     ap.add_argument("--verify-mode", type=int, default=0, help="0 = RLC groups with fallback, 1 = per-partial checks")
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
@@ -269,51 +271,60 @@ def main():
     device = local % max(1, torch.cuda.device_count())
     e = eng.Engine(device, slots=max(args.inflight, 1), verify_mode=args.verify_mode, rlc_group=args.rlc_group,
                    rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot)
-    # `inflight` independent 10k-DV batches stay resident, each in its own
-    # engine slot (own HBM arena + own streams); step k replays batch
-    # k mod inflight, so consecutive steps overlap on the GPU exactly as
-    # back-to-back tbg_submit calls of a serving node do.
+    # `inflight` engine slots each hold `merge` independent 10k-DV batches
+    # submitted together (tbg_submit_group: one device batch, one launch per
+    # kernel for all of them) and stay resident; the timed region replays the
+    # slots round-robin, so `merge` steps run per launch and `inflight`
+    # launches overlap -- what back-to-back submits of a serving node do.
+    M = max(1, args.merge)
+    if args.steps % M or args.warmup % M:
+        sys.exit(f"bench.py: --steps and --warmup must be multiples of --merge ({M})")
     batches, tickets = [], []
     pcie_ms = None
     for j in range(args.inflight):
-        b = make_batch(e, args.dvs, args.t, args.n, seed=args.seed + 1000 * rank + j, inject=args.inject)
-        ticket = e.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
-                          duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
-        first = e.collect(ticket)
-        if pcie_ms is None:
-            pcie_ms = e.timings()["total"]
-        if not batch_exact(first, b, eng):
-            print(json.dumps({"error": "parity check failed on the bench batch"}), file=sys.stderr)
-            sys.exit(2)
-        batches.append(b)
-        tickets.append(ticket)
+        group = [make_batch(e, args.dvs, args.t, args.n, seed=args.seed + 1000 * rank + M * j + k, inject=args.inject)
+                 for k in range(M)]
+        ts = e.submit_group(eng.OP_VERIFY_AGGREGATE, [
+            dict(duty_first=b.duty_first, sigs=b.sigs, identifiers=b.identifiers, msgs=(b.msg_data, b.msg_off),
+                 duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold) for b in group])
+        for b, t in zip(group, ts):
+            first = e.collect(t)
+            if pcie_ms is None:
+                pcie_ms = e.timings()["total"]
+            if not batch_exact(first, b, eng):
+                print(json.dumps({"error": "parity check failed on the bench batch"}), file=sys.stderr)
+                sys.exit(2)
+        batches.append(group)
+        tickets.append(ts[0])
 
     if args.warmup:
-        e.replay_multi(tickets, args.warmup)
+        e.replay_multi(tickets, args.warmup // M)
     kernel_ms = {}
 
     def step_fn(k):
-        kernel_ms.update(e.replay_multi(tickets, k))
+        kernel_ms.update(e.replay_multi(tickets, k // M))
 
     elapsed, _ = timed_steps(step_fn, args.steps, ws)
-    # outputs of the timed replays must still be exact
-    for b, ticket in zip(batches, tickets):
-        again = e.fetch(ticket, b.n_dv, b.n_dv * b.n)
-        assert batch_exact(again, b, eng)
-    b = batches[0]
+    # outputs of the timed replays must still be exact (every batch of every slot)
+    for group, t0 in zip(batches, tickets):
+        for k, b in enumerate(group):
+            again = e.fetch(t0 + k, b.n_dv, b.n_dv * b.n)
+            assert batch_exact(again, b, eng)
+    b = batches[0][0]
+    flat = [x for g in batches for x in g]
 
     units = args.dvs * args.steps * ws
     value = units / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # Isolated pass (untimed): one resident batch alone on the GPU, per-stage
-    # HIP events on its stream -- the per-launch durations the roofline uses
-    # (under 8-way pipelining every stage shares the CUs with 7 other batches).
+    # Isolated pass (untimed): one resident slot (`merge` batches) alone on the
+    # GPU, per-stage HIP events on its stream -- the per-launch durations the
+    # roofline uses (pipelined, every stage shares the CUs with the others).
     iso = e.replay(tickets[0], 1)
     # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
     roofline_isolated, roofline = stage_rooflines(work_model(), iso, args, value / ws)
     # (reuses the engine's slots: after the replays and the isolated pass)
-    api = api_pipeline(e, eng, batches, args.inflight, args.api_batches) if args.api_batches else None
+    api = api_pipeline(e, eng, flat, args.inflight, args.api_batches) if args.api_batches else None
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "DV-duties/s (n verifies + 1 aggregate each)",
@@ -325,7 +336,8 @@ def main():
                                 if args.workload == "config2" else
                                 f"config4: {args.t}-of-{args.n}, {args.dvs}-DV shard per GPU of the 1M-DV batch"),
                    "partials_per_step_per_gpu": args.dvs * args.n, "parallelism": f"shard{ws}",
-                   "inflight_batches": args.inflight, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
+                   "inflight_launches": args.inflight, "batches_per_launch": M,
+                   "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),
         "api_pipeline": api,

@@ -37,10 +37,20 @@ constexpr int kChainEvents = 11;
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-struct Slot {
-  bool busy = false;
-  bool collecting = false;  // a blocking tbg_collect waits on `done` outside the context mutex
+// One caller batch inside a slot: tbg_submit_group packs several batches into
+// one device batch (one launch per kernel for all of them); each keeps its
+// own ticket and its slice of the outputs.
+struct Part {
   tbg_ticket ticket = 0;
+  uint32_t d0 = 0, nd = 0, p0 = 0, np = 0;
+  bool pending = false;     // not collected yet
+  bool collecting = false;  // a blocking tbg_collect waits on the slot outside the context mutex
+};
+
+struct Slot {
+  bool busy = false;        // some part is still pending
+  std::vector<Part> parts;
+  tbg_ticket ticket = 0;    // first part's ticket (LRU order of the slots)
   uint32_t op = 0, n_duties = 0, n_partials = 0, n_msgs = 0;
   // pinned host staging
   uint8_t* h_in = nullptr;
@@ -335,10 +345,40 @@ static int validate(const tbg_batch* b) {
   return TBG_OK;
 }
 
-int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
-  if (!c || !ticket) return TBG_E_INVALID_ARG;
-  int rc = validate(b);
-  if (rc != TBG_OK) return rc;
+// The slot and part a ticket names.  want_busy: the part must be pending
+// (collect / poll) or the slot idle (replay / fetch of a collected batch).
+static Slot* find_ticket(tbg_ctx* c, tbg_ticket t, bool want_pending, Part** part) {
+  for (auto& x : c->slots)
+    for (auto& q : x.parts)
+      if (q.ticket == t && (want_pending ? q.pending : !x.busy)) {
+        if (part) *part = &q;
+        return &x;
+      }
+  return nullptr;
+}
+
+int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) { return tbg_submit_group(c, &b, 1, ticket); }
+
+int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches, tbg_ticket* tickets) {
+  if (!c || !bs || !tickets || n_batches == 0) return TBG_E_INVALID_ARG;
+  int rc;
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    if ((rc = validate(bs[k])) != TBG_OK) return rc;
+    if (bs[k]->op != bs[0]->op) return TBG_E_INVALID_ARG;  // one kernel chain per device batch
+  }
+  const uint32_t op = bs[0]->op;
+  const bool verify = op != TBG_OP_AGGREGATE;
+  uint64_t nd64 = 0, np64 = 0, nm64 = 0, mb64 = 0;
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    nd64 += bs[k]->n_duties;
+    np64 += bs[k]->n_partials;
+    if (verify) {
+      nm64 += bs[k]->n_msgs;
+      mb64 += bs[k]->msg_off[bs[k]->n_msgs];
+    }
+  }
+  if (np64 > 0x7FFFFFFFull || nd64 > 0x7FFFFFFFull || nm64 > 0x7FFFFFFFull || mb64 > 0xFFFFFFFFull)
+    return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   // Least recently used free slot: a collected batch stays resident (for
@@ -348,9 +388,8 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
     if (!x.busy && (!s || x.ticket < s->ticket)) s = &x;
   if (!s) return TBG_E_BUSY;
 
-  const bool verify = b->op != TBG_OP_AGGREGATE;
-  const uint32_t nd = b->n_duties, np = b->n_partials, nm = verify ? b->n_msgs : 0;
-  const size_t msg_bytes = verify ? b->msg_off[nm] : 0;
+  const uint32_t nd = (uint32_t)nd64, np = (uint32_t)np64, nm = (uint32_t)nm64;
+  const size_t msg_bytes = (size_t)mb64;
 
   // ---- input arena layout (16-byte aligned sections) ----
   size_t o = 0;
@@ -390,8 +429,8 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   size_t w_dvl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_dvlines = sec(G > 1 ? 4ull * LINES_WORDS * nd : 0);
   size_t w_pl = sec(verify ? 4ull * np : 0);
-  size_t w_aacc = sec(b->op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
-  size_t w_alist = sec(b->op != TBG_OP_VERIFY ? 4ull * nd : 0);
+  size_t w_aacc = sec(op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
+  size_t w_alist = sec(op != TBG_OP_VERIFY ? 4ull * nd : 0);
   size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
   size_t w_pst = sec(4ull * np);
   size_t w_dst = sec(4ull * nd);
@@ -404,27 +443,51 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   if ((rc = grow_device(&s->d_in, &s->d_in_cap, in_bytes)) != TBG_OK) return rc;
   if ((rc = grow_device(&s->d_work, &s->d_work_cap, work_bytes)) != TBG_OK) return rc;
 
+  // ---- pack: batch k's duties / partials / messages follow batch k-1's,
+  // every index rebased by the running offsets ----
   uint8_t* h = s->h_in;
-  if (msg_bytes) memcpy(h + o_msgs, b->msgs, msg_bytes);
-  if (verify) {
-    memcpy(h + o_msg_off, b->msg_off, 4ull * (nm + 1));
-    memcpy(h + o_duty_msg, b->duty_msg, 4ull * nd);
-    memcpy(h + o_pk, b->pubkey_ids, 4ull * np);
-  }
-  memcpy(h + o_duty_first, b->duty_first, 4ull * (nd + 1));
-  if (b->op == TBG_OP_VERIFY_AGGREGATE) memcpy(h + o_thr, b->duty_threshold, 4ull * nd);
-  else memset(h + o_thr, 0, 4ull * nd);
+  uint32_t* msg_off = (uint32_t*)(h + o_msg_off);
+  uint32_t* duty_msg = (uint32_t*)(h + o_duty_msg);
+  uint32_t* duty_first = (uint32_t*)(h + o_duty_first);
+  uint32_t* thr = (uint32_t*)(h + o_thr);
   uint32_t* pd = (uint32_t*)(h + o_pduty);
-  for (uint32_t d = 0; d < nd; ++d)
-    for (uint32_t j = b->duty_first[d]; j < b->duty_first[d + 1]; ++j) pd[j] = d;
-  if (np) {
-    memcpy(h + o_sigs, b->sigs, 96ull * np);
-    memcpy(h + o_ids, b->identifiers, np);
+  uint32_t D = 0, P = 0, M = 0, MB = 0;
+  std::vector<Part> parts(n_batches);
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    const tbg_batch* b = bs[k];
+    const uint32_t bnd = b->n_duties, bnp = b->n_partials, bnm = verify ? b->n_msgs : 0;
+    if (verify) {
+      const uint32_t bmb = b->msg_off[bnm];
+      if (bmb) memcpy(h + o_msgs + MB, b->msgs, bmb);
+      for (uint32_t m = 0; m < bnm; ++m) msg_off[M + m] = MB + b->msg_off[m];
+      for (uint32_t d = 0; d < bnd; ++d) duty_msg[D + d] = M + b->duty_msg[d];
+      memcpy(h + o_pk + 4ull * P, b->pubkey_ids, 4ull * bnp);
+      MB += bmb;
+    }
+    for (uint32_t d = 0; d < bnd; ++d) {
+      duty_first[D + d] = P + b->duty_first[d];
+      for (uint32_t j = b->duty_first[d]; j < b->duty_first[d + 1]; ++j) pd[P + j] = D + d;
+    }
+    if (op == TBG_OP_VERIFY_AGGREGATE) memcpy(thr + D, b->duty_threshold, 4ull * bnd);
+    else memset(thr + D, 0, 4ull * bnd);
+    if (bnp) {
+      memcpy(h + o_sigs + 96ull * P, b->sigs, 96ull * bnp);
+      memcpy(h + o_ids + P, b->identifiers, bnp);
+    }
+    parts[k].d0 = D;
+    parts[k].nd = bnd;
+    parts[k].p0 = P;
+    parts[k].np = bnp;
+    D += bnd;
+    P += bnp;
+    M += bnm;
   }
+  duty_first[nd] = np;
+  if (verify) msg_off[nm] = MB;
 
   DevBatch B;
   memset(&B, 0, sizeof(B));
-  B.op = b->op;
+  B.op = op;
   B.n_duties = nd;
   B.n_partials = np;
   B.n_msgs = nm;
@@ -495,25 +558,28 @@ int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) {
   HIP_TRY(hipMemcpyAsync(s->h_out, dw + w_out, out_bytes, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipEventRecord(s->done, st));
 
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    parts[k].ticket = c->next_ticket++;
+    parts[k].pending = true;
+    tickets[k] = parts[k].ticket;
+  }
+  s->parts = std::move(parts);
   s->busy = true;
-  s->ticket = c->next_ticket++;
-  s->op = b->op;
+  s->ticket = s->parts[0].ticket;
+  s->op = op;
   s->n_duties = nd;
   s->n_partials = np;
   s->n_msgs = nm;
   s->out_bytes = out_bytes;
   s->B = B;
   s->w_out = w_out;
-  *ticket = s->ticket;
   return TBG_OK;
 }
 
 int tbg_poll(tbg_ctx* c, tbg_ticket t) {
   if (!c) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  Slot* s = nullptr;
-  for (auto& x : c->slots)
-    if (x.busy && x.ticket == t) { s = &x; break; }
+  Slot* s = find_ticket(c, t, true, nullptr);
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
   hipError_t q = hipEventQuery(s->done);
@@ -521,43 +587,54 @@ int tbg_poll(tbg_ctx* c, tbg_ticket t) {
   return q == hipSuccess ? TBG_OK : TBG_E_DEVICE;
 }
 
-int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg, int block) {
-  if (!c) return TBG_E_INVALID_ARG;
-  std::unique_lock<std::mutex> lk(c->mu);
-  Slot* s = nullptr;
-  for (auto& x : c->slots)
-    if (x.busy && x.ticket == t) { s = &x; break; }
-  if (!s || s->collecting) return TBG_E_TICKET;
-  HIP_TRY(hipSetDevice(c->device));
-  hipError_t q = hipEventQuery(s->done);
-  if (q == hipErrorNotReady) {
-    if (!block) return TBG_E_PENDING;
-    // Wait without the context mutex: other threads keep submitting and
-    // polling meanwhile.  `collecting` keeps this slot (busy) out of every
-    // other submit / collect until the wait is over.
-    s->collecting = true;
-    hipEvent_t done = s->done;
-    int dev = c->device;
-    lk.unlock();
-    (void)hipSetDevice(dev);  // the HIP current device is per thread
-    q = hipEventSynchronize(done);
-    lk.lock();
-    s->collecting = false;
-  }
-  if (q != hipSuccess) {
-    s->busy = false;
-    return TBG_E_DEVICE;
-  }
+// A part's slice of the slot's (pinned) output image.
+static void copy_part(const Slot* s, const Part& q, int32_t* pst, int32_t* dst, uint8_t* agg) {
   const uint32_t np = s->n_partials, nd = s->n_duties;
   size_t o = 0;
   auto sec = [&](size_t bytes) { size_t at = o; o = align_up(o + bytes, 16); return at; };
   size_t o_pst = sec(4ull * np), o_dst = sec(4ull * nd), o_agg = sec(96ull * nd);
-  if (pst) memcpy(pst, s->h_out + o_pst, 4ull * np);
-  if (dst) memcpy(dst, s->h_out + o_dst, 4ull * nd);
-  if (agg) memcpy(agg, s->h_out + o_agg, 96ull * nd);
+  if (pst) memcpy(pst, s->h_out + o_pst + 4ull * q.p0, 4ull * q.np);
+  if (dst) memcpy(dst, s->h_out + o_dst + 4ull * q.d0, 4ull * q.nd);
+  if (agg) memcpy(agg, s->h_out + o_agg + 96ull * q.d0, 96ull * q.nd);
+}
+
+static void part_done(Slot* s, Part* q) {
+  q->pending = false;
+  bool any = false;
+  for (const auto& x : s->parts) any |= x.pending;
+  s->busy = any;
+}
+
+int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg, int block) {
+  if (!c) return TBG_E_INVALID_ARG;
+  std::unique_lock<std::mutex> lk(c->mu);
+  Part* q = nullptr;
+  Slot* s = find_ticket(c, t, true, &q);
+  if (!s || q->collecting) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  hipError_t e = hipEventQuery(s->done);
+  if (e == hipErrorNotReady) {
+    if (!block) return TBG_E_PENDING;
+    // Wait without the context mutex: other threads keep submitting and
+    // polling meanwhile.  The slot stays busy (this part is pending) and
+    // `collecting` keeps a second collect of the same ticket out.
+    q->collecting = true;
+    hipEvent_t done = s->done;
+    int dev = c->device;
+    lk.unlock();
+    (void)hipSetDevice(dev);  // the HIP current device is per thread
+    e = hipEventSynchronize(done);
+    lk.lock();
+    q->collecting = false;
+  }
+  if (e != hipSuccess) {
+    part_done(s, q);
+    return TBG_E_DEVICE;
+  }
+  copy_part(s, *q, pst, dst, agg);
   chain_times(s->ev, s->ms);
   memcpy(c->last_ms, s->ms, sizeof(c->last_ms));
-  s->busy = false;
+  part_done(s, q);
   return TBG_OK;
 }
 
@@ -573,8 +650,7 @@ int tbg_replay_multi(tbg_ctx* c, const tbg_ticket* tickets, uint32_t n_tickets, 
   std::lock_guard<std::mutex> lk(c->mu);
   std::vector<Slot*> sl(n_tickets, nullptr);
   for (uint32_t j = 0; j < n_tickets; ++j) {
-    for (auto& x : c->slots)
-      if (!x.busy && x.ticket == tickets[j]) sl[j] = &x;
+    sl[j] = find_ticket(c, tickets[j], false, nullptr);
     if (!sl[j]) return TBG_E_TICKET;
     for (uint32_t k = 0; k < j; ++k)
       if (sl[k] == sl[j]) return TBG_E_INVALID_ARG;
@@ -618,29 +694,20 @@ int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms8) { return tb
 int tbg_fetch(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* agg) {
   if (!c) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  Slot* s = nullptr;
-  for (auto& x : c->slots)
-    if (!x.busy && x.ticket == t) { s = &x; break; }
+  Part* q = nullptr;
+  Slot* s = find_ticket(c, t, false, &q);
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemcpyAsync(s->h_out, s->d_work + s->w_out, s->out_bytes, hipMemcpyDeviceToHost, s->st));
   HIP_TRY(hipStreamSynchronize(s->st));
-  const uint32_t np = s->n_partials, nd = s->n_duties;
-  size_t o = 0;
-  auto sec = [&](size_t bytes) { size_t at = o; o = align_up(o + bytes, 16); return at; };
-  size_t o_pst = sec(4ull * np), o_dst = sec(4ull * nd), o_agg = sec(96ull * nd);
-  if (pst) memcpy(pst, s->h_out + o_pst, 4ull * np);
-  if (dst) memcpy(dst, s->h_out + o_dst, 4ull * nd);
-  if (agg) memcpy(agg, s->h_out + o_agg, 96ull * nd);
+  copy_part(s, *q, pst, dst, agg);
   return TBG_OK;
 }
 
 int tbg_fetch_stats(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
   if (!c || !out4) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  Slot* s = nullptr;
-  for (auto& x : c->slots)
-    if (!x.busy && x.ticket == t) { s = &x; break; }
+  Slot* s = find_ticket(c, t, false, nullptr);
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
   uint32_t cnt[CNT_WORDS] = {0, 0, 0, 0};

@@ -142,6 +142,17 @@ class Engine:
         self._keep[t.value] = (nd, np_)
         return t.value
 
+    def submit_group(self, op, batches):
+        """Several batches (dicts of submit()'s arguments) as one device batch
+        (tbg_submit_group); one ticket per batch."""
+        built = [self._batch(op, **b) for b in batches]
+        arr = (ctypes.POINTER(_native.TbgBatch) * len(built))(*[ctypes.pointer(b) for b, _, _, _ in built])
+        t = np.zeros(len(built), dtype=np.uint64)
+        self._check(self._lib.tbg_submit_group(self._h, arr, len(built), _ptr(t)), "tbg_submit_group")
+        for ticket, (_, _, nd, np_) in zip(t.tolist(), built):
+            self._keep[ticket] = (nd, np_)
+        return t.tolist()
+
     def collect(self, ticket, block=True):
         nd, np_ = self._keep[ticket]
         ps = np.zeros(np_, dtype=np.int32)

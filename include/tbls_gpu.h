@@ -128,6 +128,17 @@ uint32_t tbg_pubkey_count(const tbg_ctx* ctx);
 /* Enqueue a batch (copies every input); returns a ticket. */
 int tbg_submit(tbg_ctx* ctx, const tbg_batch* batch, tbg_ticket* ticket);
 
+/* Enqueue several batches (same op) as ONE device batch: they are packed
+ * back to back (indices rebased) and every kernel of the chain runs once
+ * over all of them, so concurrent callers' batches fill the GPU together
+ * instead of queueing small launches on separate streams (the call site
+ * coalesces what arrives within its window -- parsigex peers, validatorapi
+ * submitters, parsigdb threshold hits).  tickets[k] names batch k: collect /
+ * poll / fetch it as usual; the slot is reused once every ticket has been
+ * collected.  tbg_replay / tbg_fetch_stats of any of the tickets act on the
+ * whole device batch. */
+int tbg_submit_group(tbg_ctx* ctx, const tbg_batch* const* batches, uint32_t n_batches, tbg_ticket* tickets);
+
 /* Collect a batch: partial_status [n_partials], duty_status [n_duties],
  * agg96 [n_duties * 96] (any may be NULL).  block = 0 polls (TBG_E_PENDING
  * while running, nothing consumed).  A blocking collect waits WITHOUT the

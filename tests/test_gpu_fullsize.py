@@ -197,3 +197,31 @@ def test_g1_pubkey_rejections_match_oracle(engine):
     bad = bytes.fromhex(next(v["pk"] for v in vecs if v["expect"] == "err_subgroup"))
     with pytest.raises(tbls.TblsError, match="unmarshal pubkey"):
         tbls.wire_pubshares({b"dv0": good[:2], b"dv1": [good[2], bad]}, engine)
+
+
+def test_submit_group_matches_single_batches(engine):
+    """tbg_submit_group packs several callers' batches into one device batch:
+    every ticket's statuses and aggregates equal that batch submitted alone
+    (index rebasing of duties, partials and messages), including a mixed
+    batch whose messages are shared within it, and a single-duty batch."""
+    from charon_amd import engine as eng
+    from tools.workload import make_batch, make_mixed_batch
+    parts = [make_batch(engine, 700, 3, 4, seed=71, inject=0.02), make_mixed_batch(engine, 900, seed=72, inject=0.02),
+             make_batch(engine, 1, 7, 10, seed=73), make_batch(engine, 333, 5, 7, seed=74, inject=0.05)]
+    args = [dict(duty_first=b.duty_first, sigs=b.sigs, identifiers=b.identifiers, msgs=(b.msg_data, b.msg_off),
+                 duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold) for b in parts]
+    tickets = engine.submit_group(eng.OP_VERIFY_AGGREGATE, args)
+    assert len(set(tickets)) == len(parts)
+    # collect out of order
+    got = {t: engine.collect(t) for t in reversed(tickets)}
+    for b, a, t in zip(parts, args, tickets):
+        alone = engine.run(eng.OP_VERIFY_AGGREGATE, **a)
+        g = got[t]
+        assert np.array_equal(g.partial_status, alone.partial_status)
+        assert np.array_equal(g.duty_status, alone.duty_status)
+        assert np.array_equal(g.agg, alone.agg)
+        ok = g.duty_status == 0
+        assert np.array_equal(ok, b.expect_ok) and np.array_equal(g.agg[ok], b.group_sig[ok])
+    # an empty group is refused (and nothing is left pending)
+    with pytest.raises(eng.EngineError):
+        engine.submit_group(eng.OP_VERIFY_AGGREGATE, [])
