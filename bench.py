@@ -123,7 +123,7 @@ def stage_mads(wm, args):
     """Algorithmic u32 mul-adds per launch of each stage for one clean batch
     (work model of tools/count_work.py: RLC group G = 16, chunk C = 4)."""
     m = wm["mads"]
-    nd, n = args.dvs * max(1, args.merge), args.n  # one launch covers `merge` batches
+    nd, n = args.dvs * max(1, getattr(args, "merge", 1)), args.n  # one launch covers `merge` batches
     np_ = nd * n
     G = wm.get("rlc_schedule", {}).get("group", 16)
     ng = (nd + G - 1) // G
