@@ -25,24 +25,27 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# The engine keeps several batches in flight, one HIP stream each; the HIP
-# runtime multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
-# default), and streams sharing a queue serialise.  It is read once, at HIP
-# initialisation, so it is set before anything touches the GPU (the Go host
-# process sets it in its environment).
+# GPU_MAX_HW_QUEUES (hardware queues per process, HIP's default 4) is read
+# once, at HIP initialisation.  The engine no longer needs more than the
+# default: concurrent batches are packed into one device batch per launch
+# (tbg_submit_group), so a few streams fill the GPU.  --hw-queues still sets
+# it (before anything touches the GPU) for comparisons.
 def _hw_queues(argv):
-    v = "16"
+    v = None  # default: leave the environment alone (HIP's own default is 4)
     for i, a in enumerate(argv):
         if a == "--hw-queues" and i + 1 < len(argv):
             v = argv[i + 1]
         elif a.startswith("--hw-queues="):
             v = a.split("=", 1)[1]
+    if v is None:
+        return None
     if not v.isdigit() or not 1 <= int(v) <= 32:  # HIP refuses > 32; checked before HIP initialises
         sys.exit(f"bench.py: --hw-queues must be an integer in 1..32, got {v!r}")
     return v
 
 
-os.environ["GPU_MAX_HW_QUEUES"] = _hw_queues(sys.argv)
+if _hw_queues(sys.argv) is not None:
+    os.environ["GPU_MAX_HW_QUEUES"] = _hw_queues(sys.argv)
 
 METRIC = "verified+aggregated 3-of-4 threshold BLS sigs/sec at 1/2/4/8 MI355X"
 # Measured on MI355X by tools/microbench/valu_rates.hip (2 waves/SIMD, 8
@@ -189,33 +192,41 @@ def cpu_baseline(batch, seconds: float):
     return run_cpu_baseline(batch, seconds)
 
 
-def api_pipeline(e, eng, batches, inflight, n_batches):
+def api_pipeline(e, eng, batches, inflight, n_batches, merge):
     """Side measurement of the product path: n_batches batches pushed through
-    tbg_submit / tbg_collect with up to `inflight` outstanding (what a serving
-    node does), host packing into pinned staging, H2D, the kernel chain, D2H
-    and the unpacking all inside the clock.  Not the headline (inputs are not
-    HBM-resident); every result is checked."""
+    tbg_submit_group (`merge` at a time, as a coalescing call site would) and
+    tbg_collect, with up to `inflight` groups outstanding: host packing into
+    pinned staging, H2D, the kernel chain, D2H and the unpacking all inside
+    the clock.  Not the headline (inputs are not HBM-resident); every result
+    is checked."""
     import collections
     pending = collections.deque()
     done = 0
     ok = True
-    t0 = time.perf_counter()
-    for k in range(n_batches):
-        if len(pending) >= inflight:
-            t, b = pending.popleft()
+    groups = [batches[k:k + merge] for k in range(0, n_batches, merge)]
+
+    def drain_one():
+        nonlocal done, ok
+        ts, grp = pending.popleft()
+        for t, b in zip(ts, grp):
             ok &= batch_exact(e.collect(t), b, eng)
             done += b.n_dv
-        b = batches[k % len(batches)]
-        t = e.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
-                     duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
-        pending.append((t, b))
+
+    t0 = time.perf_counter()
+    for k in range(len(groups)):
+        if len(pending) >= inflight:
+            drain_one()
+        grp = [batches[(k * merge + j) % len(batches)] for j in range(merge)]
+        ts = e.submit_group(eng.OP_VERIFY_AGGREGATE, [
+            dict(duty_first=b.duty_first, sigs=b.sigs, identifiers=b.identifiers, msgs=(b.msg_data, b.msg_off),
+                 duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold) for b in grp])
+        pending.append((ts, grp))
     while pending:
-        t, b = pending.popleft()
-        ok &= batch_exact(e.collect(t), b, eng)
-        done += b.n_dv
+        drain_one()
     dt = time.perf_counter() - t0
-    return {"value": round(done / dt, 2), "unit": "DV-duties/s", "batches": n_batches, "inflight": inflight,
-            "exact": bool(ok), "path": "tbg_submit + tbg_collect (pinned staging, H2D, chain, D2H)"}
+    return {"value": round(done / dt, 2), "unit": "DV-duties/s", "batches": done // batches[0].n_dv,
+            "batches_per_submit": merge, "inflight": inflight, "exact": bool(ok),
+            "path": "tbg_submit_group + tbg_collect (pinned staging, H2D, chain, D2H)"}
 
 
 def batch_exact(res, b, eng):
@@ -232,16 +243,16 @@ def batch_exact(res, b, eng):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=24)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--dvs", type=int, default=10000)
     ap.add_argument("--t", type=int, default=3)
     ap.add_argument("--n", type=int, default=4)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--inflight", type=int, default=8, help="engine slots replayed round-robin (launches in flight)")
-    ap.add_argument("--merge", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=3, help="engine slots replayed round-robin (launches in flight)")
+    ap.add_argument("--merge", type=int, default=16,
                     help="10k-DV batches per slot, submitted together as one device batch (tbg_submit_group)")
     ap.add_argument("--verify-mode", type=int, default=0, help="0 = RLC groups with fallback, 1 = per-partial checks")
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
@@ -249,17 +260,18 @@ def main():
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
     ap.add_argument("--inject", type=float, default=0.0,
                     help="fraction of partials replaced by invalid ones (side measurement; the headline is 0)")
-    ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (read at HIP init)")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (read at HIP init); default: the environment's / HIP's 4")
     ap.add_argument("--workload", choices=["config2", "config4"], default="config2",
                     help="config2: 10k 3-of-4 DVs per step (the headline); config4: each GPU's 125k-DV shard of "
                          "the 1M-DV 3-of-4 batch of BASELINE config 4")
-    ap.add_argument("--api-batches", type=int, default=16,
+    ap.add_argument("--api-batches", type=int, default=96,
                     help="batches pushed through the product path (tbg_submit / tbg_collect, host packing and PCIe "
                          "included) for the api_pipeline side key; 0 skips it")
     args = ap.parse_args()
     if args.workload == "config4":
         args.dvs, args.t, args.n = 125000, 3, 4
-        args.inflight = min(args.inflight, 2)  # ~19 GB of HBM per resident 125k-DV batch
+        args.inflight, args.merge = min(args.inflight, 2), 1  # ~19 GB of HBM per resident 125k-DV batch
 
     ws, rank, local = dist_setup()
     from charon_amd import engine as eng
@@ -277,8 +289,6 @@ def main():
     # slots round-robin, so `merge` steps run per launch and `inflight`
     # launches overlap -- what back-to-back submits of a serving node do.
     M = max(1, args.merge)
-    if args.steps % M or args.warmup % M:
-        sys.exit(f"bench.py: --steps and --warmup must be multiples of --merge ({M})")
     batches, tickets = [], []
     pcie_ms = None
     for j in range(args.inflight):
@@ -297,12 +307,24 @@ def main():
         batches.append(group)
         tickets.append(ts[0])
 
+    def plan(n):
+        """Launches for exactly n steps: full launches of M batches round-robin
+        over the slots, then one launch of the first n mod M batches of the next
+        slot (a prefix of a packed device batch is a batch of its own)."""
+        full, rem = divmod(n, M)
+        ts = [tickets[k % len(tickets)] for k in range(full)]
+        ps = [0] * full
+        if rem:
+            ts.append(tickets[full % len(tickets)])
+            ps.append(rem)
+        return ts, ps
+
     if args.warmup:
-        e.replay_multi(tickets, args.warmup // M)
+        e.replay_plan(*plan(args.warmup))
     kernel_ms = {}
 
     def step_fn(k):
-        kernel_ms.update(e.replay_multi(tickets, k // M))
+        kernel_ms.update(e.replay_plan(*plan(k)))
 
     elapsed, _ = timed_steps(step_fn, args.steps, ws)
     # outputs of the timed replays must still be exact (every batch of every slot)
@@ -324,7 +346,7 @@ def main():
     # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
     roofline_isolated, roofline = stage_rooflines(work_model(), iso, args, value / ws)
     # (reuses the engine's slots: after the replays and the isolated pass)
-    api = api_pipeline(e, eng, flat, args.inflight, args.api_batches) if args.api_batches else None
+    api = api_pipeline(e, eng, flat, args.inflight, args.api_batches, M) if args.api_batches else None
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "DV-duties/s (n verifies + 1 aggregate each)",
@@ -337,7 +359,7 @@ def main():
                                 f"config4: {args.t}-of-{args.n}, {args.dvs}-DV shard per GPU of the 1M-DV batch"),
                    "partials_per_step_per_gpu": args.dvs * args.n, "parallelism": f"shard{ws}",
                    "inflight_launches": args.inflight, "batches_per_launch": M,
-                   "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])},
+                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),
         "api_pipeline": api,

@@ -177,6 +177,8 @@ SIGNATURES = {
                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "tbg_submit_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    "tbg_replay_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                       ctypes.c_void_p]),
     "tbg_multi_init": (ctypes.c_int, [ctypes.POINTER(TbgConfig), ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.POINTER(ctypes.c_void_p)]),
     "tbg_multi_destroy": (None, [ctypes.c_void_p]),

@@ -42,7 +42,7 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // own ticket and its slice of the outputs.
 struct Part {
   tbg_ticket ticket = 0;
-  uint32_t d0 = 0, nd = 0, p0 = 0, np = 0;
+  uint32_t d0 = 0, nd = 0, p0 = 0, np = 0, m0 = 0, nm = 0;
   bool pending = false;     // not collected yet
   bool collecting = false;  // a blocking tbg_collect waits on the slot outside the context mutex
 };
@@ -478,6 +478,8 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
     parts[k].nd = bnd;
     parts[k].p0 = P;
     parts[k].np = bnp;
+    parts[k].m0 = M;
+    parts[k].nm = bnm;
     D += bnd;
     P += bnp;
     M += bnm;
@@ -645,39 +647,48 @@ int tbg_run(tbg_ctx* c, const tbg_batch* b, int32_t* pst, int32_t* dst, uint8_t*
   return tbg_collect(c, t, pst, dst, agg, 1);
 }
 
-int tbg_replay_multi(tbg_ctx* c, const tbg_ticket* tickets, uint32_t n_tickets, uint32_t iters, float* ms8) {
-  if (!c || !tickets || n_tickets == 0 || iters == 0) return TBG_E_INVALID_ARG;
+int tbg_replay_plan(tbg_ctx* c, const tbg_ticket* tickets, const uint32_t* n_parts, uint32_t n_launches, float* ms8) {
+  if (!c || !tickets || n_launches == 0) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  std::vector<Slot*> sl(n_tickets, nullptr);
-  for (uint32_t j = 0; j < n_tickets; ++j) {
-    sl[j] = find_ticket(c, tickets[j], false, nullptr);
-    if (!sl[j]) return TBG_E_TICKET;
-    for (uint32_t k = 0; k < j; ++k)
-      if (sl[k] == sl[j]) return TBG_E_INVALID_ARG;
+  std::vector<Slot*> sl(n_launches, nullptr);
+  std::vector<DevBatch> bs(n_launches);
+  for (uint32_t k = 0; k < n_launches; ++k) {
+    sl[k] = find_ticket(c, tickets[k], false, nullptr);
+    if (!sl[k]) return TBG_E_TICKET;
+    // A prefix of the packed device batch is itself a batch: batch j's
+    // duties, partials and messages all follow batch j-1's.
+    DevBatch B = sl[k]->B;
+    const uint32_t np = n_parts ? n_parts[k] : 0;
+    if (np > sl[k]->parts.size()) return TBG_E_INVALID_ARG;
+    if (np && np < sl[k]->parts.size()) {
+      const Part& last = sl[k]->parts[np - 1];
+      B.n_duties = last.d0 + last.nd;
+      B.n_partials = last.p0 + last.np;
+      B.n_msgs = last.m0 + last.nm;
+    }
+    bs[k] = B;
   }
   HIP_TRY(hipSetDevice(c->device));
-  std::vector<hipEvent_t> ev((size_t)kChainEvents * iters);
+  std::vector<hipEvent_t> ev((size_t)kChainEvents * n_launches);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   int rc = TBG_OK;
-  // Round-robin over the resident batches: launch k runs on the streams of
-  // slot k mod n_tickets, so up to n_tickets batches are in flight at once.
-  for (uint32_t k = 0; k < iters && rc == TBG_OK; ++k) {
-    Slot* s = sl[k % n_tickets];
-    rc = launch_chain(c, *s, s->B, ev.data() + (size_t)kChainEvents * k);
-  }
-  for (uint32_t j = 0; j < n_tickets; ++j) {
-    if (hipStreamSynchronize(sl[j]->st) != hipSuccess) rc = TBG_E_DEVICE;
-    if (hipStreamSynchronize(sl[j]->st2) != hipSuccess) rc = TBG_E_DEVICE;
+  // Launch k on the streams of its slot: launches of different slots are in
+  // flight together, launches of one slot run in order.
+  for (uint32_t k = 0; k < n_launches && rc == TBG_OK; ++k)
+    rc = launch_chain(c, *sl[k], bs[k], ev.data() + (size_t)kChainEvents * k);
+  for (uint32_t k = 0; k < n_launches; ++k) {
+    if (hipStreamSynchronize(sl[k]->st) != hipSuccess) rc = TBG_E_DEVICE;
+    if (hipStreamSynchronize(sl[k]->st2) != hipSuccess) rc = TBG_E_DEVICE;
   }
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (rc == TBG_OK) {
-    for (uint32_t k = 0; k < iters; ++k) {
+    for (uint32_t k = 0; k < n_launches; ++k) {
       float m[8];
       chain_times(ev.data() + (size_t)kChainEvents * k, m);
       for (int j = 0; j < 7; ++j) acc[j] += m[j];
     }
     // wall time: first launch's start to the latest chain end
-    for (uint32_t k = (iters > n_tickets ? iters - n_tickets : 0); k < iters; ++k) {
+    for (uint32_t k = 0; k < n_launches; ++k) {
       float w = 0;
       hipEventElapsedTime(&w, ev[0], ev[(size_t)kChainEvents * k + 9]);
       if (w > acc[7]) acc[7] = w;
@@ -687,6 +698,13 @@ int tbg_replay_multi(tbg_ctx* c, const tbg_ticket* tickets, uint32_t n_tickets, 
   }
   for (auto& e : ev) hipEventDestroy(e);
   return rc;
+}
+
+int tbg_replay_multi(tbg_ctx* c, const tbg_ticket* tickets, uint32_t n_tickets, uint32_t iters, float* ms8) {
+  if (!c || !tickets || n_tickets == 0 || iters == 0) return TBG_E_INVALID_ARG;
+  std::vector<tbg_ticket> plan(iters);
+  for (uint32_t k = 0; k < iters; ++k) plan[k] = tickets[k % n_tickets];  // round-robin over the resident batches
+  return tbg_replay_plan(c, plan.data(), nullptr, iters, ms8);
 }
 
 int tbg_replay(tbg_ctx* c, tbg_ticket t, uint32_t iters, float* ms8) { return tbg_replay_multi(c, &t, 1, iters, ms8); }

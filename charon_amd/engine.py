@@ -189,6 +189,15 @@ class Engine:
         self._check(self._lib.tbg_replay_multi(self._h, _ptr(t), len(t), iters, _ptr(ms)), "tbg_replay_multi")
         return dict(zip(TIMING_KEYS, ms.tolist()))
 
+    def replay_plan(self, tickets, n_parts=None):
+        """Launch k re-runs the first n_parts[k] batches (0: all) of the
+        resident device batch of tickets[k] (tbg_replay_plan)."""
+        t = np.ascontiguousarray(np.asarray(tickets, dtype=np.uint64))
+        p = None if n_parts is None else np.ascontiguousarray(np.asarray(n_parts, dtype=np.uint32))
+        ms = np.zeros(8, dtype=np.float32)
+        self._check(self._lib.tbg_replay_plan(self._h, _ptr(t), _ptr(p), len(t), _ptr(ms)), "tbg_replay_plan")
+        return dict(zip(TIMING_KEYS, ms.tolist()))
+
     def fetch(self, ticket, n_duties, n_partials) -> BatchResult:
         ps = np.zeros(n_partials, dtype=np.int32)
         ds = np.zeros(n_duties, dtype=np.int32)

@@ -163,6 +163,11 @@ int tbg_replay(tbg_ctx* ctx, tbg_ticket ticket, uint32_t iters, float* ms8);
  * streams, so up to n_tickets batches are in flight at once (the pipelined
  * throughput of back-to-back submits).  ms8[7] is the wall time. */
 int tbg_replay_multi(tbg_ctx* ctx, const tbg_ticket* tickets, uint32_t n_tickets, uint32_t iters, float* ms8);
+/* Replay an explicit plan: launch k re-runs the first n_parts[k] caller
+ * batches (0 or NULL: all) of the resident device batch tickets[k] belongs
+ * to (a prefix of a packed tbg_submit_group batch is a batch of its own), on
+ * that slot's streams; launches of different slots are in flight together. */
+int tbg_replay_plan(tbg_ctx* ctx, const tbg_ticket* tickets, const uint32_t* n_parts, uint32_t n_launches, float* ms8);
 int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
 /* Verification work of a collected batch's last run: out4 = [level-1 groups,
  * duties re-checked alone (level 2), partials checked one by one (level 3),

@@ -214,6 +214,13 @@ def test_submit_group_matches_single_batches(engine):
     assert len(set(tickets)) == len(parts)
     # collect out of order
     got = {t: engine.collect(t) for t in reversed(tickets)}
+    # prefix replays of the packed device batch (tbg_replay_plan) leave every
+    # ticket's results intact (before other submits reuse the slot)
+    engine.replay_plan([tickets[0], tickets[0], tickets[0]], [1, 3, 0])
+    for b, t in zip(parts, tickets):
+        again = engine.fetch(t, b.n_dv, int(b.duty_first[-1]))
+        assert np.array_equal(again.partial_status, got[t].partial_status)
+        assert np.array_equal(again.agg, got[t].agg)
     for b, a, t in zip(parts, args, tickets):
         alone = engine.run(eng.OP_VERIFY_AGGREGATE, **a)
         g = got[t]
