@@ -48,9 +48,11 @@ if _hw_queues(sys.argv) is not None:
     os.environ["GPU_MAX_HW_QUEUES"] = _hw_queues(sys.argv)
 
 METRIC = "verified+aggregated 3-of-4 threshold BLS sigs/sec at 1/2/4/8 MI355X"
-# Measured on MI355X by tools/microbench/valu_rates.hip (2 waves/SIMD, 8
-# independent chains): v_mad_u64_u32 = 32.1 T lane-ops/s.  See DESIGN.md.
-PEAK_MAD_TOPS = 32.1
+# Best measured v_mad_u64_u32 rate on MI355X (tools/microbench/valu_rates.hip,
+# profiles/r02/valu_rates.txt: 19.0 / 32.8 / 32.2 / 30.4 T lane-ops/s at
+# 1 / 2 / 4 / 8 waves per SIMD); the 4-cycle issue model gives 39.3 T at
+# 2.4 GHz (256 CU x 4 SIMD x 32 lanes / 2).  See DESIGN.md.
+PEAK_MAD_TOPS = 32.8
 
 
 def dist_setup():
@@ -112,13 +114,13 @@ def work_model():
 
 # Stages of the kernel chain (tbg_last_timings order) and their kernels.
 STAGE_KERNELS = {
-    "decode": ["k_decode_sigs"],
-    "hash": ["k_hash_msgs"],
-    "combine": ["k_rlc_partial", "k_rlc_duty_sum", "k_rlc_group_lines"],
+    "decode": ["k_decode_sigs", "k_subgroup_sigs"],
+    "hash": ["k_hash_map", "k_hash_clear", "k_hash_affine"],
+    "combine": ["k_rlc_partial2", "k_rlc_duty_sum", "k_rlc_group_lines"],
     "h_lines": ["k_lines_h"],
     "verify": ["k_rlc_miller_chunks", "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_duty_lines",
                "k_rlc_check_duties", "k_lines_sig_list", "k_verify_list"],
-    "aggregate": ["k_lagrange", "k_aggregate"],
+    "aggregate": ["k_lagrange", "k_aggregate", "k_aggregate_finish"],
 }
 
 
@@ -150,39 +152,60 @@ def traffic_model():
     return None
 
 
-def stage_rooflines(wm, iso, args, value):
+def stage_traffic(tm, stage, batches):
+    """HBM bytes per launch of `batches` batches for a stage's kernels, from
+    the committed PMC passes (FETCH_SIZE x 2, the gfx950 correction of
+    MI355X_MICROARCH.md, + WRITE_SIZE), scaled from the PMC run's launch size."""
+    if not tm:
+        return None
+    kk = tm.get("kernels", {})
+    names = [k for k in STAGE_KERNELS[stage] if k in kk]
+    if not names:
+        return None
+    per_batch = sum(1024 * (2 * kk[k].get("FETCH_SIZE_KB_per_launch", 0) + kk[k].get("WRITE_SIZE_KB_per_launch", 0))
+                    for k in names) / max(1, tm.get("batches_per_launch", 1))
+    return int(per_batch * batches)
+
+
+def stage_rooflines(wm, iso, timed, args, value, steps):
+    """roofline: the dominant stage of the timed region -- its algorithmic
+    mul-adds over the timed steps / the summed HIP-event durations of its
+    launches (on the slot streams they ran on); with launches in flight
+    together those durations include sharing the CUs, so this is a lower
+    bound.  roofline_isolated: the same stage, one launch alone.
+    roofline_pipeline: the whole chain, work / wall time."""
     if not wm or args.t != 3 or args.n != 4:
-        return None, None
-    mads = stage_mads(wm, args)
-    stage = max(mads, key=lambda k: iso.get(k, 0.0))  # dominant stage of the isolated batch
-    ms = iso[stage]
-    achieved = mads[stage] / (ms * 1e-3) / 1e12
-    traffic = None
+        return None, None, None
+    M = max(1, getattr(args, "merge", 1))
+    per_batch = {k: v / M for k, v in stage_mads(wm, args).items()}
     tm = traffic_model()
-    if tm:
-        kk = tm.get("kernels", {})
-        if all(k in kk for k in STAGE_KERNELS[stage][:2]):
-            traffic = int(sum(1024 * (kk[k].get("FETCH_SIZE_KB_per_launch", 0) + kk[k].get("WRITE_SIZE_KB_per_launch", 0))
-                              for k in STAGE_KERNELS[stage] if k in kk))
+    stage = max(per_batch, key=lambda k: timed.get(k, 0.0))
+    total_ms = timed[stage]
+    ach = per_batch[stage] * steps / (total_ms * 1e-3) / 1e12
+    n_launch = -(-steps // M)
     roofline = {"bound": "valu-int-mul", "kernel": f"{stage} stage: " + " + ".join(STAGE_KERNELS[stage][:3]),
-                "achieved": round(achieved, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
-                "frac": round(achieved / PEAK_MAD_TOPS, 4), "traffic": traffic,
-                "algorithmic_mads_per_launch": int(mads[stage]), "launch_ms": round(ms, 3)}
+                "achieved": round(ach, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
+                "frac": round(ach / PEAK_MAD_TOPS, 4), "traffic": stage_traffic(tm, stage, M),
+                "algorithmic_mads_per_launch": int(per_batch[stage] * M), "launches": n_launch,
+                "avg_launch_ms": round(total_ms / max(1, steps / M), 3),
+                "measured": "HIP events around the stage on its slot's stream, timed region"}
+    iso_stage = max(per_batch, key=lambda k: iso.get(k, 0.0))
+    ach_i = per_batch[iso_stage] * M / (iso[iso_stage] * 1e-3) / 1e12
+    isolated = {"bound": "valu-int-mul", "kernel": f"{iso_stage} stage: " + " + ".join(STAGE_KERNELS[iso_stage][:3]),
+                "achieved": round(ach_i, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
+                "frac": round(ach_i / PEAK_MAD_TOPS, 4), "traffic": stage_traffic(tm, iso_stage, M),
+                "algorithmic_mads_per_launch": int(per_batch[iso_stage] * M), "launch_ms": round(iso[iso_stage], 3),
+                "batches_per_launch": M}
     unit = wm["mads"]["unit_3of4_rlc"]
     ach_p = value * unit / 1e12
-    step_traffic = None
-    if tm:
-        step_traffic = int(sum(1024 * (v.get("FETCH_SIZE_KB_per_launch", 0) + v.get("WRITE_SIZE_KB_per_launch", 0))
-                               for k, v in tm.get("kernels", {}).items() if any(k in ks for ks in STAGE_KERNELS.values())))
-    pipeline = {"bound": "valu-int-mul",
-                "kernel": "the whole kernel chain of one step (batches pipelined, kernels of 8 batches overlap, so "
-                          "per-kernel durations are not separable in the timed region)",
+    pipeline = {"bound": "valu-int-mul", "kernel": "the whole kernel chain (launches in flight together)",
                 "achieved": round(ach_p, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
-                "frac": round(ach_p / PEAK_MAD_TOPS, 4), "traffic": step_traffic,
+                "frac": round(ach_p / PEAK_MAD_TOPS, 4),
+                "traffic": (sum(stage_traffic(tm, s_, 1) or 0 for s_ in STAGE_KERNELS) or None) if tm else None,
                 "work_per_unit_mads": unit,
                 "reference_schedule_mads_per_unit": wm["mads"]["unit_3of4_single_lane_schedule"],
                 "reference_schedule_equivalent_tmads": round(value * wm["mads"]["unit_3of4_single_lane_schedule"] / 1e12, 3)}
-    return roofline, pipeline
+    return roofline, isolated, pipeline
 
 
 def cpu_baseline(batch, seconds: float):
@@ -344,7 +367,8 @@ def main():
     # roofline uses (pipelined, every stage shares the CUs with the others).
     iso = e.replay(tickets[0], 1)
     # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
-    roofline_isolated, roofline = stage_rooflines(work_model(), iso, args, value / ws)
+    roofline, roofline_isolated, roofline_pipeline = stage_rooflines(work_model(), iso, kernel_ms, args, value / ws,
+                                                                     args.steps)
     # (reuses the engine's slots: after the replays and the isolated pass)
     api = api_pipeline(e, eng, flat, args.inflight, args.api_batches, M) if args.api_batches else None
 
@@ -366,6 +390,7 @@ def main():
         "isolated_batch_ms": {k: round(v, 3) for k, v in iso.items()},
         "roofline": roofline,
         "roofline_isolated": roofline_isolated,
+        "roofline_pipeline": roofline_pipeline,
         "cpu_baseline": None,
     }
     if rank == 0 and not args.no_cpu and ws == 1:

@@ -58,11 +58,15 @@ def test_roofline_fields_from_work_model():
     import bench
     wm = bench.work_model()
     assert wm is not None
-    args = argparse.Namespace(dvs=10000, t=3, n=4)
-    iso = {"decode": 2.8, "hash": 6.6, "combine": 8.4, "h_lines": 2.5, "verify": 11.2, "aggregate": 0.8}
-    stage, pipe = bench.stage_rooflines(wm, iso, args, 1.0e6)
-    assert stage["kernel"].startswith("verify stage")
-    assert abs(stage["achieved"] - stage["algorithmic_mads_per_launch"] / 11.2e-3 / 1e12) < 1e-2
+    args = argparse.Namespace(dvs=10000, t=3, n=4, merge=16)
+    iso = {"decode": 22.8, "hash": 16.6, "combine": 28.4, "h_lines": 6.5, "verify": 41.2, "aggregate": 2.8}
+    timed = {k: 3 * 1.5 * v for k, v in iso.items()}  # 3 launches of 16 batches, 1.5x slower when shared
+    stage, iso_r, pipe = bench.stage_rooflines(wm, iso, timed, args, 1.0e6, 48)
+    assert stage["kernel"].startswith("verify stage") and iso_r["kernel"].startswith("verify stage")
+    # timed-region form: work of the 48 steps over the summed launch time
+    assert abs(stage["achieved"] - stage["algorithmic_mads_per_launch"] * 3 / (timed["verify"] * 1e-3) / 1e12) < 1e-2
+    assert abs(iso_r["achieved"] - iso_r["algorithmic_mads_per_launch"] / 41.2e-3 / 1e12) < 1e-2
+    assert abs(iso_r["achieved"] / stage["achieved"] - 1.5) < 1e-3
     assert abs(pipe["achieved"] - 1.0e6 * wm["mads"]["unit_3of4_rlc"] / 1e12) < 1e-2
     assert 0 < pipe["frac"] < 1
 
