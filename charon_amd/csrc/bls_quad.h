@@ -228,6 +228,36 @@ __device__ TBG_QUAD_FN Fp4 quad_final_exp(const Fp4& f) {
   return quad_mul(c, t3);
 }
 
+// Kernel-inline forms of the final exponentiation for the level-1 group
+// check (k_rlc_group_final, the per-group hot path): the 5 x 63 cyclotomic
+// squarings run inline in the kernel's own loop instead of as out-of-line
+// calls, each of which passed its Fp4 operands through the scratch stack
+// (4.1 GB of scratch write-back per 160k-DV launch, profiles/r02/
+// traffic_merge16.json).  The rare products stay out of line.  Call these
+// from a kernel body only: kernels are not affected by the long-branch
+// return-address hazard of out-of-line loops (see _native.py).
+TBG_DEV Fp4 quad_pow_xabs_in(const Fp4& a) {
+  Fp4 r = a;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    r = quad_cyc_sqr_in(r);
+    if ((X_ABS >> i) & 1) r = quad_mul(r, a);
+  }
+  return r;
+}
+TBG_DEV Fp4 quad_pow_x_in(const Fp4& a) { return quad_conj(quad_pow_xabs_in(a)); }
+TBG_DEV Fp4 quad_final_exp_in(const Fp4& f) {
+  Fp4 t = quad_mul(quad_conj(f), quad_inv(f));
+  t = quad_mul(quad_frob(quad_frob(t)), t);
+  Fp4 a = quad_mul(quad_pow_x_in(t), quad_conj(t));
+  a = quad_mul(quad_pow_x_in(a), quad_conj(a));
+  Fp4 b = quad_mul(quad_pow_x_in(a), quad_frob(a));
+  Fp4 c = quad_mul(quad_pow_x_in(quad_pow_x_in(b)), quad_frob(quad_frob(b)));
+  c = quad_mul(c, quad_conj(b));
+  Fp4 t3 = quad_mul(quad_cyc_sqr(t), t);
+  return quad_mul(c, t3);
+}
+
 // true on every lane iff the quad's element is 1
 TBG_DEV bool quad_is_one(const Fp4& A) {
   int q = quad_lane();

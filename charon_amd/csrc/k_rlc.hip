@@ -147,7 +147,7 @@ __device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
 // Level 1, Miller part: one quad per (group, chunk of rlc_chunk duties); the
 // group's S pair rides in chunk 0.  Chunks share nothing but the final
 // exponentiation, so a group's pairs are spread over several quads.
-__global__ void TBG_LAUNCH k_rlc_miller_chunks(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
@@ -199,7 +199,7 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
   const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nch * g;
   Fp4 f = quad_load(base);
   for (uint32_t c = 1; c < nch; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
-  f = quad_final_exp(quad_conj(f));
+  f = quad_final_exp_in(quad_conj(f));
   bool ok = quad_is_one(f);
   if (lead) B.grp_state[g] = ok ? GRP_OK : GRP_FAIL;
 }

@@ -27,6 +27,9 @@ constexpr int kBlock = 64;
 #ifndef TBG_DECODE_WAVES
 #define TBG_DECODE_WAVES 2  // k_decode_sigs (square roots only)
 #endif
+#ifndef TBG_CHUNK_WAVES
+#define TBG_CHUNK_WAVES 1   // k_rlc_miller_chunks (quad Fp12, one wave per SIMD)
+#endif
 #define TBG_LAUNCH_N(w) __launch_bounds__(64, w)
 inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
