@@ -144,20 +144,26 @@ __device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
   return A;
 }
 
-// Level 1, Miller part: one quad per (group, chunk of rlc_chunk duties); the
-// group's S pair rides in chunk 0.  Chunks share nothing but the final
-// exponentiation, so a group's pairs are spread over several quads.
+// Level 1, Miller part: one quad per (group, chunk of rlc_chunk duties),
+// plus one quad per group for the group's S pair alone (chunk index nch).
+// Chunks share nothing but the final exponentiation, so a group's pairs are
+// spread over several quads -- and because the P pairs of a chunk are kept
+// apart from S, a failed group can re-check its chunks (level 1.5) from these
+// same products with only S_c's Miller loop added.
 __global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
-  uint32_t nch = (G + C - 1) / C;
+  uint32_t nch = (G + C - 1) / C, nq = nch + 1;
   uint32_t qd = t >> 2;
-  if (qd >= n_groups * nch) return;
-  uint32_t g = qd / nch, c = qd % nch;
-  if (B.grp_state[g] != GRP_LINES) return;
+  if (qd >= n_groups * nq) return;
+  uint32_t g = qd / nq, c = qd % nq;
+  // a group whose S sum degenerated (GRP_FAIL here) still gets its P-chunk
+  // products: level 1.5 re-checks its chunks from them
+  const int32_t gs = B.grp_state[g];
+  if (gs == GRP_EMPTY || (gs == GRP_FAIL && c == nch)) return;
   uint32_t gd1 = min(g * G + G, B.n_duties);
-  uint32_t d0 = g * G + c * C, d1 = min(d0 + C, gd1);
+  uint32_t d0 = g * G + c * C, d1 = c == nch ? d0 : min(d0 + C, gd1);
   const uint32_t* ls = B.grp_lines + (size_t)LINES_WORDS * g;
   Fp4 f = quad_one();
   int idx = 0;
@@ -165,7 +171,7 @@ __global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
     if (b != 62) f = quad_sqr_in(f);
     int steps = ((X_ABS >> b) & 1) ? 2 : 1;
     for (int s = 0; s < steps; ++s, ++idx) {
-      if (c == 0) f = quad_line_folded<true>(f, ls, idx);
+      if (c == nch) f = quad_line_folded<true>(f, ls, idx);
       for (uint32_t d = d0; d < d1; ++d) {
         if (B.dv_state[d] != RLC_COMBINED) continue;
         uint32_t m = B.duty_msg[d];
@@ -179,12 +185,12 @@ __global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
 }
 
 // Level 1, final part: one quad per group multiplies its chunks' products
-// and runs the one final exponentiation of the group.
+// (the S chunk included) and runs the one final exponentiation of the group.
 __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
-  uint32_t nch = (G + C - 1) / C;
+  uint32_t nq = (G + C - 1) / C + 1;
   uint32_t g = t >> 2;
   if (g >= n_groups) return;
   const bool lead = (t & 3) == 0;
@@ -192,13 +198,13 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
   uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
   for (uint32_t d = d0; d < d1; ++d) {
     if (B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] != 0) {
-      if (lead) B.grp_state[g] = GRP_FAIL;  // resolved per duty
+      if (lead) B.grp_state[g] = GRP_FAIL;  // resolved per chunk / duty
       return;
     }
   }
-  const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nch * g;
+  const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nq * g;
   Fp4 f = quad_load(base);
-  for (uint32_t c = 1; c < nch; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
+  for (uint32_t c = 1; c < nq; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
   f = quad_final_exp_in(quad_conj(f));
   bool ok = quad_is_one(f);
   if (lead) B.grp_state[g] = ok ? GRP_OK : GRP_FAIL;
@@ -213,7 +219,13 @@ __device__ __forceinline__ void rlc_push_partials(const DevBatch& B, uint32_t d)
     if (rlc_candidate(B, i)) B.part_list[atomicAdd(&B.counters[CNT_PARTIALS], 1u)] = i;
 }
 
-// After level 1 (one thread per duty): accept, split into level 2, or go to level 3.
+// A duty that level 1.5 / 2 may combine: COMBINED and its H(m) usable.
+__device__ __forceinline__ bool rlc_combinable(const DevBatch& B, uint32_t d) {
+  return B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] == 0;
+}
+
+// After level 1 (one thread per duty): accept, split into level 1.5 (the
+// failed group's chunks), or go to level 3.
 __global__ void TBG_LAUNCH k_rlc_resolve_groups(DevBatch B) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= B.n_duties) return;
@@ -221,10 +233,76 @@ __global__ void TBG_LAUNCH k_rlc_resolve_groups(DevBatch B) {
   if (st == RLC_NONE) return;
   if (st == RLC_EACH) { rlc_push_partials(B, d); return; }
   if (B.h_status[B.duty_msg[d]] != 0) { rlc_mark(B, d, TBG_PS_INVALID); return; }
-  int32_t gs = B.grp_state[d / B.rlc_group];
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk;
+  const uint32_t g = d / G;
+  int32_t gs = B.grp_state[g];
   if (gs == GRP_OK) { rlc_mark(B, d, TBG_PS_VALID); return; }
-  if (B.rlc_group > 1) B.dv_list[atomicAdd(&B.counters[CNT_DUTIES], 1u)] = d;
-  else rlc_push_partials(B, d);
+  if (G == 1) { rlc_push_partials(B, d); return; }
+  // the chunk goes to level 1.5 once: pushed by its first combinable duty
+  const uint32_t c = (d - g * G) / C, dc0 = g * G + c * C;
+  for (uint32_t e = dc0; e < d; ++e)
+    if (rlc_combinable(B, e)) return;
+  const uint32_t nch = (G + C - 1) / C;
+  B.chunk_list[atomicAdd(&B.counters[CNT_CHUNKS], 1u)] = g * nch + c;
+}
+
+// Level 1.5 lines: one thread per listed chunk: S_c = sum of its combinable
+// duties' S_d, Miller lines with -g1 folded in.  A degenerate S_c (point at
+// infinity) flags the list entry: its duties go straight to level 2.
+constexpr uint32_t CHUNK_DEGENERATE = 0x80000000u;
+__global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= B.counters[CNT_CHUNKS]) return;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C;
+  const uint32_t qc = B.chunk_list[k], g = qc / nch, c = qc % nch;
+  const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
+  G2J S = jac_inf<Fp2>();
+  for (uint32_t d = d0; d < d1; ++d)
+    if (rlc_combinable(B, d)) S = jac_add(S, B.dv_s[d]);
+  G2A Sa;
+  if (!jac_to_aff(S, Sa)) {
+    B.chunk_list[k] = qc | CHUNK_DEGENERATE;
+    return;
+  }
+  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.chunk_lines + (size_t)LINES_WORDS * k);
+}
+
+// Level 1.5 check: one quad per listed chunk: its stored P-pair product
+// times the Miller loop of S_c, one final exponentiation.  Pass -> the
+// chunk's duties are valid; fail -> its duties go to level 2 (or, for a
+// chunk with a single duty, its partials straight to level 3).
+__global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t k = t >> 2;
+  if (k >= B.counters[CNT_CHUNKS]) return;
+  const bool lead = (t & 3) == 0;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C, nq = nch + 1;
+  const uint32_t entry = B.chunk_list[k], qc = entry & ~CHUNK_DEGENERATE, g = qc / nch, c = qc % nch;
+  const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
+  bool ok = false;
+  if (!(entry & CHUNK_DEGENERATE)) {
+    const uint32_t* ls = B.chunk_lines + (size_t)LINES_WORDS * k;
+    Fp4 f = quad_one();
+    int idx = 0;
+    for (int b = 62; b >= 0; --b) {
+      if (b != 62) f = quad_sqr(f);
+      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+      for (int s = 0; s < steps; ++s, ++idx) f = quad_line_folded(f, ls, idx);
+    }
+    f = quad_mul(f, quad_load(B.chunk_f + (size_t)3 * QUAD_WORDS * (g * nq + c)));
+    f = quad_final_exp(quad_conj(f));
+    ok = quad_is_one(f);
+  }
+  if (!lead) return;
+  uint32_t n = 0;
+  for (uint32_t d = d0; d < d1; ++d) n += rlc_combinable(B, d) ? 1u : 0u;
+  for (uint32_t d = d0; d < d1; ++d) {
+    if (!rlc_combinable(B, d)) continue;
+    if (ok) rlc_mark(B, d, TBG_PS_VALID);
+    else if (n == 1 && !(entry & CHUNK_DEGENERATE)) rlc_push_partials(B, d);  // level 2 would repeat this check
+    else B.dv_list[atomicAdd(&B.counters[CNT_DUTIES], 1u)] = d;
+  }
 }
 
 // Level 2 lines: one thread per listed duty.
@@ -337,10 +415,12 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
   if (B.rlc_group != 0) {
     uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
-    TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups * (nch + 1)), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_group_final, grid_for(4 * n_groups), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
+      TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_check_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_duty_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_check_duties, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
     }

@@ -419,7 +419,9 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   const uint32_t nch = G ? (G + C - 1) / C : 0;
   size_t w_pp = sec(G ? sizeof(G1J) * (size_t)np : 0);
   size_t w_ps = sec(G ? sizeof(G2J) * (size_t)np : 0);
-  size_t w_cf = sec(G ? 4ull * 3 * 4 * NL * ng * nch : 0);
+  size_t w_cf = sec(G ? 4ull * 3 * 4 * NL * ng * (nch + 1) : 0);
+  size_t w_cl = sec(G > 1 ? 4ull * ng * nch : 0);
+  size_t w_clines = sec(G > 1 ? 4ull * LINES_WORDS * ng * nch : 0);
   size_t w_dvp = sec(G ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_dvs = sec(G ? sizeof(G2J) * (size_t)nd : 0);
   size_t w_dvst = sec(G ? 4ull * nd : 0);
@@ -536,6 +538,8 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.part_p = (G1J*)(dw + w_pp);
   B.part_s = (G2J*)(dw + w_ps);
   B.chunk_f = (uint32_t*)(dw + w_cf);
+  B.chunk_list = (uint32_t*)(dw + w_cl);
+  B.chunk_lines = (uint32_t*)(dw + w_clines);
   B.dv_p = (G1A*)(dw + w_dvp);
   B.dv_s = (G2J*)(dw + w_dvs);
   B.dv_state = (int32_t*)(dw + w_dvst);

@@ -59,7 +59,10 @@ struct DevBatch {
   G1J* part_p;            // [n_partials] r_i pk_i
   G2J* part_s;            // [n_partials] r_i sig_i
   uint32_t rlc_chunk;     // duties per level-1 Miller chunk (quads per group = ceil(G / chunk))
-  uint32_t* chunk_f;      // [n_groups * chunks][3][4 NL] Miller products of the chunks (quad layout)
+  uint32_t* chunk_f;      // [n_groups * (chunks + 1)][3][4 NL] Miller products of the chunks (quad layout);
+                          // chunk index `chunks` of a group is its S pair alone
+  uint32_t* chunk_list;   // [n_groups * chunks] level-1.5 chunks of failed groups (group * chunks + c)
+  uint32_t* chunk_lines;  // [n_groups * chunks][LINES_WORDS] lines of S_c, by chunk-list position
   G1A* dv_p;              // [n_duties] sum r_i pk_i (affine)
   G2J* dv_s;              // [n_duties] sum r_i sig_i
   int32_t* dv_state;      // [n_duties] RLC_*
@@ -80,7 +83,7 @@ struct DevBatch {
 
 enum RlcState : int32_t { RLC_NONE = 0, RLC_COMBINED = 1, RLC_EACH = 2 };
 enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3 };
-enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_WORDS = 4 };
+enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_WORDS = 4 };
 
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {
