@@ -135,10 +135,56 @@ TBG_NI bool lagrange_encode(const uint8_t* ids, int k, int me, uint32_t (&w)[8])
 // defer_D != nullptr: an integer-mode sum with denominator D > 1 is returned
 // before the [1/D] multiplication and *defer_D = D (else *defer_D = 1); the
 // caller finishes it with tss_div_den.
-TBG_HD G2J tss_div_den(const G2J& acc, uint64_t D) {
+//
+// [k] P for a 255-bit k on G2 as a 4-way MSM of 64-bit digits: psi(P) = [x] P
+// on G2 and x < 0, so [|x|^i] P = (-psi)^i (P) and with the base-|x| digits
+// k = d0 + d1 |x| + d2 |x|^2 + d3 |x|^3 (0 <= d_i < |x|; r < |x|^4)
+//   [k] P = [d0] P + [d1] (-psi(P)) + [d2] psi^2(P) + [d3] (-psi^3(P)).
+// 64 doublings instead of 255; the GPU spreads the four terms over a lane quad
+// (k_aggregate_finish).  P must have order r (decoded points are subgroup-checked).
+TBG_HD void base_x_digits(const uint32_t (&w)[8], uint64_t (&d)[4]) {
+  uint32_t q[8];
+  for (int j = 0; j < 8; ++j) q[j] = w[j];
+  for (int i = 0; i < 3; ++i) {  // q, d_i = divmod(q, |x|), restoring division MSB first
+    uint64_t rem = 0;
+    for (int b = 255; b >= 0; --b) {
+      const uint32_t bit = (q[b >> 5] >> (b & 31)) & 1u;
+      const uint64_t top = rem >> 63;
+      rem = (rem << 1) | bit;  // the true value is < 2|x| < 2^65: subtract mod 2^64
+      const bool ge = top || rem >= X_ABS;
+      if (ge) rem -= X_ABS;
+      q[b >> 5] = (q[b >> 5] & ~(1u << (b & 31))) | ((ge ? 1u : 0u) << (b & 31));
+    }
+    d[i] = rem;
+  }
+  d[3] = (uint64_t)q[0] | ((uint64_t)q[1] << 32);  // q < |x| after three divisions
+}
+// The four MSM bases: (-psi)^i (P).
+TBG_HD G2J base_x_point(const G2J& p, int i) {
+  G2J q = p;
+  for (int j = 0; j < i; ++j) q = g2_psi(q);
+  return (i & 1) ? jac_neg(q) : q;
+}
+TBG_HD G2J g2_mul_base_x(const G2J& p, const uint64_t (&d)[4]) {
+  G2J q[4];
+  for (int i = 0; i < 4; ++i) q[i] = base_x_point(p, i);
+  G2J acc = jac_inf<Fp2>();
+  for (int b = 63; b >= 0; --b) {  // Straus: one doubling chain for the four digits
+    acc = jac_dbl(acc);
+    for (int i = 0; i < 4; ++i)
+      if ((d[i] >> b) & 1) acc = jac_add(acc, q[i]);
+  }
+  return acc;
+}
+TBG_HD void inv_den_digits(uint64_t D, uint64_t (&d)[4]) {
   uint32_t dw[8];
   fr_to_words(fr_inv(fr_from_u64(D)), dw);
-  return jac_mul_words(acc, dw, 255);
+  base_x_digits(dw, d);
+}
+TBG_HD G2J tss_div_den(const G2J& acc, uint64_t D) {
+  uint64_t d[4];
+  inv_den_digits(D, d);
+  return g2_mul_base_x(acc, d);
 }
 TBG_NI G2J tss_combine(const G2A* pts, const uint32_t* lam, const uint8_t* mask, int count,
                        uint64_t* defer_D = nullptr) {

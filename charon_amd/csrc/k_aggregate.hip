@@ -91,16 +91,40 @@ __global__ void TBG_LAUNCH k_aggregate(DevBatch B) {
   agg_emit(B, d, acc);
 }
 
+__device__ __forceinline__ G2J shfl_xor_g2j(const G2J& a, int m) {
+  G2J r;
+  const Fp* src[6] = {&a.X.c0, &a.X.c1, &a.Y.c0, &a.Y.c1, &a.Z.c0, &a.Z.c1};
+  Fp* dst[6] = {&r.X.c0, &r.X.c1, &r.Y.c0, &r.Y.c1, &r.Z.c0, &r.Z.c1};
+  for (int k = 0; k < 6; ++k)
+    for (int j = 0; j < NL; ++j) dst[k]->l[j] = __shfl_xor(src[k]->l[j], m, 4);
+  return r;
+}
+
+// [1/D] acc as the 4-way base-|x| MSM of bls_tss.h, one term per lane of a
+// quad (64 doublings each instead of 255 on one lane), summed over the quad.
 __global__ void TBG_LAUNCH k_aggregate_finish(DevBatch B) {
-  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= B.counters[CNT_AGG]) return;
-  uint32_t d = B.agg_list[k];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = t >> 2;
+  const int q = (int)(t & 3);
+  if (k >= B.counters[CNT_AGG]) return;  // quad-uniform
+  const uint32_t d = B.agg_list[k];
   uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
   uint32_t j = first;
   while (j < last && !participates(B.op, B.partial_status[j])) ++j;
   const uint32_t* w = B.lam + 8ull * j;  // listed duties have a participant (k >= 2)
   uint64_t D = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
-  agg_emit(B, d, tss_div_den(B.agg_acc[d], D));
+  uint64_t dg[4];
+  inv_den_digits(D, dg);
+  const uint64_t e = q == 0 ? dg[0] : q == 1 ? dg[1] : q == 2 ? dg[2] : dg[3];
+  const G2J p = base_x_point(B.agg_acc[d], q);
+  G2J acc = jac_inf<Fp2>();
+  for (int b = 63; b >= 0; --b) {
+    acc = jac_dbl_in(acc);
+    if ((e >> b) & 1) acc = jac_add_in<Fp2, true>(acc, p);
+  }
+  acc = jac_add_in<Fp2, true>(acc, shfl_xor_g2j(acc, 1));
+  acc = jac_add_in<Fp2, true>(acc, shfl_xor_g2j(acc, 2));
+  if (q == 0) agg_emit(B, d, acc);
 }
 
 void launch_lagrange(const DevBatch& B, hipStream_t st) {
@@ -110,7 +134,7 @@ void launch_aggregate(const DevBatch& B, hipStream_t st) {
   if (B.n_duties) TBG_KLAUNCH(k_aggregate, grid_for(B.n_duties), dim3(kBlock), st, B);
 }
 void launch_aggregate_finish(const DevBatch& B, hipStream_t st) {
-  if (B.n_duties) TBG_KLAUNCH(k_aggregate_finish, grid_for(B.n_duties), dim3(kBlock), st, B);
+  if (B.n_duties) TBG_KLAUNCH(k_aggregate_finish, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

@@ -155,9 +155,14 @@ __global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
   uint32_t nch = (G + C - 1) / C, nq = nch + 1;
+  // P chunks first, then every group's S quad: S quads evaluate one line per
+  // step instead of C, and in waves of their own they finish early instead of
+  // each holding a P chunk's wave slot for its full length
   uint32_t qd = t >> 2;
   if (qd >= n_groups * nq) return;
-  uint32_t g = qd / nq, c = qd % nq;
+  const uint32_t np_q = n_groups * nch;
+  uint32_t g = qd < np_q ? qd / nch : qd - np_q, c = qd < np_q ? qd % nch : nch;
+  qd = g * nq + c;  // storage index
   // a group whose S sum degenerated (GRP_FAIL here) still gets its P-chunk
   // products: level 1.5 re-checks its chunks from them
   const int32_t gs = B.grp_state[g];
@@ -270,8 +275,7 @@ __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
 
 // Level 1.5 check: one quad per listed chunk: its stored P-pair product
 // times the Miller loop of S_c, one final exponentiation.  Pass -> the
-// chunk's duties are valid; fail -> its duties go to level 2 (or, for a
-// chunk with a single duty, its partials straight to level 3).
+// chunk's duties are valid; fail -> its duties go to level 2.
 __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t k = t >> 2;
@@ -300,8 +304,8 @@ __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
   for (uint32_t d = d0; d < d1; ++d) {
     if (!rlc_combinable(B, d)) continue;
     if (ok) rlc_mark(B, d, TBG_PS_VALID);
-    else if (n == 1 && !(entry & CHUNK_DEGENERATE)) rlc_push_partials(B, d);  // level 2 would repeat this check
-    else B.dv_list[atomicAdd(&B.counters[CNT_DUTIES], 1u)] = d;
+    else B.dv_list[atomicAdd(&B.counters[CNT_DUTIES], 1u)] = d;  // (a lone duty: level 2 repeats the
+                                                                    // check but keeps its value for 2b)
   }
 }
 
@@ -316,7 +320,15 @@ __global__ void TBG_LAUNCH k_rlc_duty_lines(DevBatch B) {
   g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.dv_lines + (size_t)LINES_WORDS * k);
 }
 
-// Level 2 check: one quad per listed duty; failures go to level 3.
+__device__ __forceinline__ uint32_t rlc_candidates(const DevBatch& B, uint32_t d) {
+  uint32_t n = 0;
+  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) n += rlc_candidate(B, i) ? 1u : 0u;
+  return n;
+}
+
+// Level 2 check: one quad per listed duty.  A failed duty with one candidate
+// is decided (the check is that partial's own, scaled by r != 0); a failed
+// duty with several keeps its final-exponentiated value A_d for level 2b.
 __global__ void TBG_LAUNCH k_rlc_check_duties(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t k = t >> 2;
@@ -339,9 +351,99 @@ __global__ void TBG_LAUNCH k_rlc_check_duties(DevBatch B) {
   }
   f = quad_final_exp(quad_conj(f));
   bool ok = quad_is_one(f);
+  if (!ok && rlc_candidates(B, d) > 1) {
+    quad_store(B.dv_fe + (size_t)3 * QUAD_WORDS * k, f);
+    if (lead) B.id_list[atomicAdd(&B.counters[CNT_IDENT], 1u)] = k;
+    return;
+  }
+  if (lead) rlc_mark(B, d, ok ? TBG_PS_VALID : TBG_PS_INVALID);
+}
+
+// Level 2b: find the invalid partial of a failed duty with one extra check
+// instead of one per partial (the exponent test of Lee, Cheon and Hong,
+// "Finding invalid signatures in pairing-based batches").  With
+// eps_i = e(pk_i, H(m)) e(-g1, s_i) (1 iff partial i is valid) and weights
+// w_i = 1..n over the candidates,
+//   A_d  = prod_i eps_i^(r_i)        (level 2's value, kept in dv_fe),
+//   A'_d = prod_i eps_i^(w_i r_i)    (this level: P' = sum w_i r_i pk_i, S' = sum w_i r_i s_i).
+// If exactly partial b is invalid, A'_d = A_d^(w_b): b is found, the others are
+// valid.  A match for any w with two or more invalid partials needs the
+// secret r_i to satisfy a fixed linear relation (probability n 2^-64, the RLC
+// bound); no match sends the duty's candidates to level 3.
+constexpr uint32_t ID_DEGENERATE = 0x80000000u;
+
+// Lines of S' and affine P', one thread per level-2b entry.  w_i = 1..n is the
+// candidate's rank from the duty's start, summed as suffix sums from its end
+// (U = sum_j T_j, T_j = sum of the last j candidates: two additions each).
+__global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= B.counters[CNT_IDENT]) return;
+  const uint32_t e = B.id_list[k], d = B.dv_list[e];
+  G1J Tp = jac_inf<Fp>(), Up = jac_inf<Fp>();
+  G2J Ts = jac_inf<Fp2>(), Us = jac_inf<Fp2>();
+  for (uint32_t i = B.duty_first[d + 1]; i-- > B.duty_first[d];) {
+    if (!rlc_candidate(B, i)) continue;
+    Tp = jac_add(Tp, B.part_p[i]);
+    Up = jac_add(Up, Tp);
+    Ts = jac_add(Ts, B.part_s[i]);
+    Us = jac_add(Us, Ts);
+  }
+  G1A Pa;
+  G2A Sa;
+  if (!jac_to_aff(Up, Pa) || !jac_to_aff(Us, Sa)) {
+    B.id_list[k] = e | ID_DEGENERATE;
+    return;
+  }
+  B.id_p[k] = Pa;
+  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.id_lines + (size_t)LINES_WORDS * k);
+}
+
+// Level 2b check: one quad per entry computes A'_d and tests A_d^w == A'_d.
+__global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t k = t >> 2;
+  if (k >= B.counters[CNT_IDENT]) return;
+  const bool lead = (t & 3) == 0;
+  const uint32_t entry = B.id_list[k], e = entry & ~ID_DEGENERATE, d = B.dv_list[e];
+  uint32_t found = 0;  // weight of the one invalid candidate; 0 = not identified
+  if (!(entry & ID_DEGENERATE)) {
+    const G1A P = B.id_p[k];
+    Fp nx = fp_reduce(fp_neg(P.x));
+    const uint32_t* ls = B.id_lines + (size_t)LINES_WORDS * k;
+    const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d];
+    Fp4 f = quad_one();
+    int idx = 0;
+    for (int b = 62; b >= 0; --b) {
+      if (b != 62) f = quad_sqr(f);
+      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+      for (int s = 0; s < steps; ++s, ++idx) {
+        f = quad_line_folded(f, ls, idx);
+        f = quad_line_at(f, lh, idx, nx, P.y);
+      }
+    }
+    const Fp4 inv_a2 = quad_final_exp(f);  // (A'_d)^-1: the conjugate is the inverse in GT
+    const Fp4 A = quad_load(B.dv_fe + (size_t)3 * QUAD_WORDS * e);
+    const uint32_t n = rlc_candidates(B, d);
+    Fp4 Aw = A;
+    for (uint32_t w = 1; w <= n; ++w) {  // quad-uniform: quad_is_one agrees on all lanes
+      if (quad_is_one(quad_mul(Aw, inv_a2))) {
+        found = w;
+        break;
+      }
+      Aw = quad_mul(Aw, A);
+    }
+  }
   if (!lead) return;
-  if (ok) rlc_mark(B, d, TBG_PS_VALID);
-  else rlc_push_partials(B, d);
+  if (!found) {
+    rlc_push_partials(B, d);
+    return;
+  }
+  uint32_t w = 0;
+  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) {
+    if (!rlc_candidate(B, i)) continue;
+    B.partial_status[i] = ++w == found ? TBG_PS_INVALID : TBG_PS_VALID;
+  }
 }
 
 // Per-partial schedule (TBG_VERIFY_EACH): every candidate goes to level 3.
@@ -423,6 +525,8 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
       TBG_KLAUNCH(k_rlc_check_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_duty_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_check_duties, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_ident_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_ident_check, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
     }
   }
   if (B.n_partials) {

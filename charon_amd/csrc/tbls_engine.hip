@@ -431,6 +431,9 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_dvl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_dvlines = sec(G > 1 ? 4ull * LINES_WORDS * nd : 0);
   size_t w_pl = sec(verify ? 4ull * np : 0);
+  size_t w_dvfe = sec(G > 1 ? 4ull * 3 * 4 * NL * nd : 0);
+  size_t w_idl = sec(G > 1 ? 4ull * nd : 0);
+  size_t w_idp = sec(G > 1 ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_aacc = sec(op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
   size_t w_alist = sec(op != TBG_OP_VERIFY ? 4ull * nd : 0);
   size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
@@ -549,6 +552,10 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.dv_list = (uint32_t*)(dw + w_dvl);
   B.dv_lines = (uint32_t*)(dw + w_dvlines);
   B.part_list = (uint32_t*)(dw + w_pl);
+  B.dv_fe = (uint32_t*)(dw + w_dvfe);
+  B.id_list = (uint32_t*)(dw + w_idl);
+  B.id_p = (G1A*)(dw + w_idp);
+  B.id_lines = B.sig_lines;  // nd <= np list positions; level 3 rewrites them after level 2b
   B.partial_status = (int32_t*)(dw + w_pst);
   B.duty_status = (int32_t*)(dw + w_dst);
   B.agg = dw + w_agg;
@@ -732,7 +739,7 @@ int tbg_fetch_stats(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
   Slot* s = find_ticket(c, t, false, nullptr);
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
-  uint32_t cnt[CNT_WORDS] = {0, 0, 0, 0};
+  uint32_t cnt[CNT_WORDS] = {};
   if (s->op != TBG_OP_AGGREGATE) {
     HIP_TRY(hipMemcpyAsync(cnt, s->B.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
     HIP_TRY(hipStreamSynchronize(s->st));

@@ -72,6 +72,11 @@ struct DevBatch {
   uint32_t* dv_list;      // [n_duties] level-2 duties
   uint32_t* dv_lines;     // [n_duties][LINES_WORDS] lines of S_d, by level-2 list position
   uint32_t* part_list;    // [n_partials] level-3 partials (sig_lines by list position)
+  uint32_t* dv_fe;        // [n_duties][3][4 NL] final-exponentiated level-2 value of failed duties (by list position)
+  uint32_t* id_list;      // [n_duties] level-2b entries: level-2 list positions of failed multi-partial duties
+  G1A* id_p;              // [n_duties] sum w_i r_i pk_i (affine), by level-2b position
+  uint32_t* id_lines;     // lines of sum w_i r_i sig_i by level-2b position: aliases sig_lines,
+                          // which level 3 only fills after level 2b has consumed them
   // recombination (k_aggregate.hip)
   G2J* agg_acc;           // [n_duties] integer-coefficient sums awaiting [1/D] (listed duties only)
   uint32_t* agg_list;     // [n_duties] duties whose Lagrange denominator D > 1
@@ -83,7 +88,7 @@ struct DevBatch {
 
 enum RlcState : int32_t { RLC_NONE = 0, RLC_COMBINED = 1, RLC_EACH = 2 };
 enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3 };
-enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_WORDS = 4 };
+enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_IDENT = 4, CNT_WORDS = 5 };
 
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {

@@ -528,3 +528,18 @@ extern "C" int hc_rlc_check_j(const uint8_t* sig96, const uint8_t* pk48, uint64_
   }
   return out;
 }
+
+// [k] P through the base-|x| digits (bls_tss.h g2_mul_base_x, the
+// k_aggregate_finish MSM) against the plain 255-bit double-and-add.  Writes
+// the four digits to d4; returns 1 on agreement.
+extern "C" int hc_base_x_check(const uint8_t* sig96, const uint32_t* k_words, uint64_t* d4) {
+  G2A s;
+  if (g2_decompress(sig96, s) != DEC_OK) return -1;
+  uint32_t w[8];
+  for (int j = 0; j < 8; ++j) w[j] = k_words[j];
+  uint64_t d[4];
+  base_x_digits(w, d);
+  for (int i = 0; i < 4; ++i) d4[i] = d[i];
+  const G2J p = jac_from_aff(s);
+  return jac_eq(g2_mul_base_x(p, d), jac_mul_words(p, w, 256)) ? 1 : 0;
+}

@@ -296,6 +296,26 @@ def test_rlc_digit_scalars_match_plain_scalar_multiplication():
         assert L.hc_rlc_check_j(sig, pk, r64, words) == 7
 
 
+def test_base_x_msm_matches_plain_scalar_multiplication():
+    """k_aggregate_finish's [1/D] as a 4-way MSM over the base-|x| digits of
+    the scalar (bls_tss.h): digits reconstruct k, each below |x|, and the MSM
+    equals the plain double-and-add, on edge and random scalars."""
+    import ctypes
+    L = lib()
+    L.hc_base_x_check.restype = ctypes.c_int
+    L.hc_base_x_check.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
+    xa = bls.X_ABS
+    sig = bls.g2_compress(tb.sign(rng.randrange(1, bls.R), b"base-x"))
+    ks = [0, 1, xa - 1, xa, xa + 1, xa ** 2, xa ** 3 - 1, xa ** 3, bls.R - 1, (bls.R + 1) // 2]
+    ks += [pow(D, -1, bls.R) for D in (2, 3, 4, 6, 8, 15, 2 ** 61 - 1)]
+    ks += [rng.randrange(bls.R) for _ in range(4)]
+    for k in ks:
+        words = (ctypes.c_uint32 * 8)(*[(k >> (32 * j)) & 0xFFFFFFFF for j in range(8)])
+        d = (ctypes.c_uint64 * 4)()
+        assert L.hc_base_x_check(sig, words, d) == 1, hex(k)
+        assert all(v < xa for v in d) and sum(v * xa ** i for i, v in enumerate(d)) == k
+
+
 def test_rlc_digit_scalars_are_distinct_mod_r():
     """Distinct digit vectors give distinct scalars (the 2^-64 soundness bound):
     |x| > 2^16 and 2^16 |x|^3 < r, checked on the extreme digit values."""
