@@ -118,8 +118,9 @@ STAGE_KERNELS = {
     "hash": ["k_hash_map", "k_hash_clear", "k_hash_affine"],
     "combine": ["k_rlc_partial2", "k_rlc_duty_sum", "k_rlc_group_lines"],
     "h_lines": ["k_lines_h"],
-    "verify": ["k_rlc_miller_chunks", "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_duty_lines",
-               "k_rlc_check_duties", "k_lines_sig_list", "k_verify_list"],
+    "verify": ["k_rlc_miller_chunks", "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_chunk_lines",
+               "k_rlc_check_chunks", "k_rlc_cident_lines", "k_rlc_cident_check", "k_rlc_ident_lines",
+               "k_rlc_ident_check", "k_lines_sig_list", "k_verify_list"],
     "aggregate": ["k_lagrange", "k_aggregate", "k_aggregate_finish"],
 }
 
@@ -392,7 +393,13 @@ def main():
         "roofline_isolated": roofline_isolated,
         "roofline_pipeline": roofline_pipeline,
         "cpu_baseline": None,
+        "host_signing_roots": None,
     }
+    if rank == 0:
+        # the host step in front of the GPU path: AttestationData -> signing
+        # root (include/tbls_ssz.h), 16 threads -- must outpace `value`
+        from tools.ssz_bench import run_rate
+        result["host_signing_roots"] = run_rate(1 << 18, 16, reps=2)
     if rank == 0 and not args.no_cpu and ws == 1:
         result["cpu_baseline"] = cpu_baseline(b, args.cpu_seconds)
     if rank == 0:

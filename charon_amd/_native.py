@@ -16,6 +16,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_PATH = os.path.join(PKG, "libtbls_gpu.so")
 HEADER = os.path.join(ROOT, "include", "tbls_gpu.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "tbls_ssz.h")]
 
 
 def _hipcc():
@@ -25,9 +26,16 @@ def _hipcc():
     raise RuntimeError("hipcc not found: cannot build libtbls_gpu.so")
 
 
+def _clangxx():
+    c = "/opt/rocm/llvm/bin/clang++"
+    if not os.path.exists(c):
+        raise RuntimeError("ROCm clang++ not found: cannot build the host units of libtbls_gpu.so")
+    return c
+
+
 def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
-                  if f.endswith((".h", ".hip"))) + [HEADER]
+                  if f.endswith((".h", ".hip", ".cpp"))) + HEADERS
 
 
 def is_stale():
@@ -47,7 +55,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
         return LIB_PATH
     from concurrent.futures import ThreadPoolExecutor
     hipcc = _hipcc()
-    units = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
+    # .hip: device + host code (hipcc); .cpp: host-only code (ROCm clang++, no offload)
+    units = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
     # one object directory per output (variants never share the product's objects)
     tag = os.path.basename(target).replace(".so", "")
     if os.path.abspath(target) != LIB_PATH:
@@ -61,13 +70,19 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     stamp = os.path.join(objdir, "flags.txt")
     same_flags = os.path.exists(stamp) and open(stamp).read() == " ".join(flags)
 
+    host_flags = ["-O3", "-std=c++17", "-fPIC"] + ["-D" + d for d in defines] + \
+        [f for f in extra_flags if f != "-Xarch_host"]
+
     def compile_unit(u):
-        obj = os.path.join(objdir, u.replace(".hip", ".o"))
+        obj = os.path.join(objdir, os.path.splitext(u)[0] + ".o")
         if same_flags and not force and os.path.exists(obj):
             t = os.path.getmtime(obj)
             if all(os.path.getmtime(d) < t for d in headers + [os.path.join(CSRC, u)]):
                 return obj  # up to date (incremental rebuild)
-        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, u), "-o", obj]
+        if u.endswith(".cpp"):
+            cmd = [_clangxx()] + host_flags + ["-c", os.path.join(CSRC, u), "-o", obj]
+        else:
+            cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, u), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
@@ -190,6 +205,13 @@ SIGNATURES = {
     "tbg_multi_collect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int]),
     "tbg_multi_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    # include/tbls_ssz.h (host code)
+    "tbg_ssz_size": (ctypes.c_uint32, [ctypes.c_uint32]),
+    "tbg_ssz_roots": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.c_uint32]),
+    "tbg_compute_domain": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]),
+    "tbg_signing_roots": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
 }
 
 _lib = None

@@ -5,12 +5,14 @@
   verify(spec, name, epoch, root, sig, pk)   signing.go:120-151
   verify_batch(spec, items)                  the batched form the batch-aware
                                              call sites use: one GPU submit
+  get_data_roots / message_signing_roots     the signing roots of a batch in
+                                             one native call (include/tbls_ssz.h)
 
 The signing root is SSZ ``hash_tree_root(SigningData{object_root, domain})``,
 i.e. SHA-256 over the two 32-byte leaves, and the domain is
 ``domain_type || hash_tree_root(ForkData{version, genesis_validators_root})[:28]``
-(consensus-specs ``compute_domain``).  Both are host work (two SHA-256
-compressions per item, negligible beside the pairing check); everything after
+(consensus-specs ``compute_domain``).  Both are host work (a few SHA-256
+compressions per item, batched in charon_amd/csrc/ssz_roots.cpp); everything after
 -- G2 decode, hash_to_G2, the pairing check -- runs on the GPU through
 ``charon_amd.tbls``.
 
@@ -117,6 +119,45 @@ def get_data_root(spec: Spec, name: str, epoch: int, root: bytes) -> bytes:
     return signing_root(root, spec.domain(name, epoch))
 
 
+def _domain_table(spec: Spec, names, epochs):
+    """Distinct domains of (name, epoch) pairs and each pair's index."""
+    table, domains, idx = {}, [], []
+    for name, e in zip(names, epochs):
+        d = spec.domain(name, e)
+        if d not in table:
+            table[d] = len(domains)
+            domains.append(d)
+        idx.append(table[d])
+    return domains, idx
+
+
+def get_data_roots(spec: Spec, name, epochs, object_roots) -> list:
+    """GetDataRoot over a batch (one native call, include/tbls_ssz.h).  `name`
+    is one domain name or one per item."""
+    from . import ssz
+    epochs = list(epochs)
+    names = [name] * len(epochs) if isinstance(name, str) else list(name)
+    roots = list(object_roots)
+    if not roots:
+        return []
+    if any(len(r) != 32 for r in roots):
+        raise SigningError("marshal signing data")
+    domains, idx = _domain_table(spec, names, epochs)
+    return ssz.signing_roots([bytes(r) for r in roots], domains, idx, kind=ssz.ROOT)
+
+
+def message_signing_roots(spec: Spec, name, epochs, objects) -> list:
+    """MessageRoot + GetDataRoot fused for typed duty objects of one kind
+    (charon_amd.ssz): the 32-byte messages their signatures cover."""
+    from . import ssz
+    objects, epochs = list(objects), list(epochs)
+    if not objects:
+        return []
+    names = [name] * len(epochs) if isinstance(name, str) else list(name)
+    domains, idx = _domain_table(spec, names, epochs)
+    return ssz.signing_roots(objects, domains, idx)
+
+
 @dataclass(frozen=True)
 class VerifyItem:
     """Arguments of one signing.Verify call."""
@@ -136,12 +177,22 @@ def verify_batch(spec: Spec, items, engine=None):
     items = list(items)
     out = [None] * len(items)
     todo, gpu_items = [], []
+    # signing roots of every well-formed item in one native batch
+    ok = []
     for i, it in enumerate(items):
         try:
-            msg = get_data_root(spec, it.domain, it.epoch, it.object_root)
+            spec.domain(it.domain, it.epoch)
+            if len(it.object_root) != 32:
+                raise SigningError("marshal signing data")
+            ok.append(i)
         except SigningError as e:
             out[i] = e
+    msgs = dict(zip(ok, get_data_roots(spec, [items[i].domain for i in ok], [items[i].epoch for i in ok],
+                                       [items[i].object_root for i in ok])))
+    for i, it in enumerate(items):
+        if out[i] is not None:
             continue
+        msg = msgs[i]
         sig = bytes(it.signature)
         if sig == _ZERO_SIG:
             out[i] = SigningError("no signature found")

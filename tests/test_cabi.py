@@ -1,5 +1,6 @@
 """The C-ABI library loads and exports every entry point include/tbls_gpu.h
-declares (no compute without a GPU), and fails loudly without a device."""
+and include/tbls_ssz.h declare (no GPU compute without a GPU), and fails
+loudly without a device."""
 import ctypes
 import os
 import re
@@ -7,11 +8,11 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "tbls_gpu.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("tbls_gpu.h", "tbls_ssz.h")]
 
 
 def declared():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:int|void|const char\s*\*|uint32_t|tbg_ctx\s*\*)\s*(tbg_\w+)\s*\(", src, re.M)))
 
 
@@ -27,7 +28,8 @@ def test_header_declares_the_boundary():
     for must in ["tbg_init", "tbg_destroy", "tbg_load_pubkeys", "tbg_submit", "tbg_collect", "tbg_run",
                  "tbg_replay", "tbg_replay_multi", "tbg_fetch", "tbg_strerror", "tbg_sign", "tbg_sk_to_pk",
                  "tbg_poll", "tbg_multi_init", "tbg_multi_submit", "tbg_multi_collect", "tbg_multi_load_pubkeys",
-                 "tbg_multi_context", "tbg_multi_layout"]:
+                 "tbg_multi_context", "tbg_multi_layout", "tbg_ssz_roots", "tbg_signing_roots",
+                 "tbg_compute_domain", "tbg_ssz_size"]:
         assert must in names
 
 

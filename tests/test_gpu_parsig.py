@@ -129,3 +129,43 @@ def test_validatorapi_batch_verify(fx, engine):
     bad = [i for i, s in enumerate(fx["sets"]) if s["peer"] == 1 and s["fault"] == "wrong_share"][0]
     items = [(pk, data) for pk, data in sets[bad][1].items()]
     assert str(parsig.verify_partial_sigs(spec, share_of.__getitem__, items, engine)) == "invalid signature"
+
+
+def test_reference_signed_objects_verify_through_native_roots(engine):
+    """MessageRoot + GetDataRoot computed by the native batch (include/tbls_ssz.h)
+    from the typed objects, then verified on the GPU: the reference's
+    attestation (validatorapi_test.go:230-289), deposit and registration
+    signatures all verify; each object with one field changed does not."""
+    from charon_amd import ssz
+    from oracle import bls12_381 as bls
+    from oracle import tbls_oracle as tb
+    H = bytes.fromhex
+    g = json.load(open(os.path.join(HERE, "golden", "ssz_vectors.json")))
+    v = g["sign_and_verify_attestation"]
+    spec = signing.Spec(forks=[(0, H(v["fork_version"]))], genesis_validators_root=H(v["genesis_validators_root"]))
+    att = ssz.AttestationData(v["slot"], v["index"], H(v["beacon_block_root"]),
+                              ssz.Checkpoint(v["source"]["epoch"], H(v["source"]["root"])),
+                              ssz.Checkpoint(v["target"]["epoch"], H(v["target"]["root"])))
+    bad_att = ssz.AttestationData(v["slot"] + 1, v["index"], att.beacon_block_root, att.source, att.target)
+    att_pk = tbls.PublicKey(bls.g1_compress(tb.sk_to_pk(int(v["secret_key"], 16))))
+    roots = signing.message_signing_roots(spec, signing.DOMAIN_BEACON_ATTESTER, [0, 0], [att, bad_att])
+    assert roots[0].hex() == v["signing_root"]
+    items = [(att_pk, roots[0], tbls.Signature(H(v["signature"]))), (att_pk, roots[1], tbls.Signature(H(v["signature"])))]
+    deps = g["deposits"]
+    dspec = signing.Spec(forks=[(0, H(deps[0]["fork_version"]))])
+    msgs = [ssz.DepositMessage(H(d["pubkey"]), H(d["withdrawal_credentials"]), d["amount"]) for d in deps]
+    msgs += [ssz.DepositMessage(m.pubkey, m.withdrawal_credentials, m.amount + 1) for m in msgs]
+    droots = signing.message_signing_roots(dspec, signing.DOMAIN_DEPOSIT, [0] * len(msgs), msgs)
+    for k, m in enumerate(msgs):
+        d = deps[k % len(deps)]
+        items.append((tbls.PublicKey(H(d["pubkey"])), droots[k], tbls.Signature(H(d["signature"]))))
+    r = g["validator_registration"]
+    reg = ssz.ValidatorRegistration(H(r["fee_recipient"]), r["gas_limit"], r["timestamp"], H(r["pubkey"]))
+    bad_reg = ssz.ValidatorRegistration(reg.fee_recipient, reg.gas_limit + 1, reg.timestamp, reg.pubkey)
+    rspec = signing.Spec(forks=[(0, H(r["fork_version"]))])
+    rroots = signing.message_signing_roots(rspec, signing.DOMAIN_APPLICATION_BUILDER, [0, 0], [reg, bad_reg])
+    for rr in rroots:
+        items.append((tbls.PublicKey(H(r["pubkey"])), rr, tbls.Signature(H(r["signature"]))))
+    got = tbls.verify_batch(items, engine)
+    n = len(deps)
+    assert got == [True, False] + [True] * n + [False] * n + [True, False]
