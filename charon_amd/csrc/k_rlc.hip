@@ -7,20 +7,25 @@
 // share pk_i:  e(pk_i, H(m_d)) == e(g1, s_i).  With secret 64-bit scalars r_i
 // (r = 1 for the first candidate of a level-1 group) drawn after the inputs are fixed,
 //
-//   level 1, group of G duties:  prod_d e(P_d, H(m_d)) * e(-g1, S) == 1,
-//            P_d = sum_i r_i pk_i,  S = sum_d S_d,  S_d = sum_i r_i s_i,
-//   level 2, one duty:           e(P_d, H(m_d)) * e(-g1, S_d) == 1,
-//   level 3, one partial:        e(pk_i, H(m_d)) * e(-g1, s_i) == 1.
+//   level 1,   group of G duties:  prod_d e(P_d, H(m_d)) * e(-g1, S) == 1,
+//              P_d = sum_i r_i pk_i,  S = sum_d S_d,  S_d = sum_i r_i s_i,
+//              run as C-duty chunks of P pairs + the S pair, one quad each;
+//   level 1.5, a failed group's chunk c: the stored P-chunk product * e(-g1, S_c);
+//   level 1.5b, a failed chunk: the exponent test finds its one bad duty;
+//   level 2b,  a bad duty: the exponent test finds its one bad partial;
+//   level 3,   one partial:        e(pk_i, H(m_d)) * e(-g1, s_i) == 1.
 //
 // A group that passes accepts all its candidates (a false accept needs the
 // scalars to hit a root of a nonzero relation: probability <= 2^-64).  A
-// group that fails is split into its duties, a duty that fails into its
-// partials, and level 3 is the exact per-item check -- so every partial's
-// verdict is the one tbls.Verify would return.  One quad of lanes runs each
-// product check (bls_quad.h) over Miller lines stored in HBM: the H(m) lines
-// are shared by all partials of a message, the -g1 factor is folded into the
-// lines of S / S_d / s_i.  Work lists for levels 2 and 3 are compacted on the
-// device (atomic counters), so a clean batch launches them over empty lists.
+// failed group is narrowed to its failed chunks, a failed chunk to its bad
+// duty, a bad duty to its bad partial; whatever the exponent tests cannot
+// pin down (two or more bad members) goes to level 3, the exact per-item
+// check -- so every partial's verdict is the one tbls.Verify would return.
+// One quad of lanes runs each product check (bls_quad.h) over Miller lines
+// stored in HBM: the H(m) lines are shared by all partials of a message, the
+// -g1 factor is folded into the lines of S / S_c / s_i.  Work lists of the
+// fallback levels are compacted on the device (atomic counters), so a clean
+// batch launches them over empty lists.
 // The P == Q case of the mixed addition doubles inline (bls_curve.h): no
 // out-of-line call inside the kernels' point loops.
 #define TBG_ADD_DBL_INLINE 1
@@ -253,7 +258,7 @@ __global__ void TBG_LAUNCH k_rlc_resolve_groups(DevBatch B) {
 
 // Level 1.5 lines: one thread per listed chunk: S_c = sum of its combinable
 // duties' S_d, Miller lines with -g1 folded in.  A degenerate S_c (point at
-// infinity) flags the list entry: its duties go straight to level 2.
+// infinity) flags the list entry: its candidates go straight to level 3.
 constexpr uint32_t CHUNK_DEGENERATE = 0x80000000u;
 __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -273,9 +278,50 @@ __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
   g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.chunk_lines + (size_t)LINES_WORDS * k);
 }
 
+__device__ __forceinline__ uint32_t rlc_candidates(const DevBatch& B, uint32_t d) {
+  uint32_t n = 0;
+  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) n += rlc_candidate(B, i) ? 1u : 0u;
+  return n;
+}
+
+// ---------------------------------------------------------- identification
+// The exponent test (Lee, Cheon and Hong, "Finding invalid signatures in
+// pairing-based batches") finds the one bad member of a failed product with
+// ONE more check instead of one per member.  For members j with values
+// eps_j (1 iff member j is valid) and weights w_j = 1..m,
+//   A  = prod_j eps_j^(r_j)        (the failed check's final-exponentiated value),
+//   A' = prod_j eps_j^(w_j r_j)    (the same check with every member scaled by w_j).
+// If exactly member b is bad, A' = A^(w_b): b is found and the others are
+// valid.  A match for some w with two or more bad members needs the secret
+// r_j to satisfy a fixed nonzero linear relation (probability m 2^-64, the
+// RLC bound); no match falls through to the next level.
+//   level 1.5b, a failed chunk (members = duties, eps = the duty's RLC product);
+//   level 2b, a failed duty (members = partials, eps = the partial's pairing check).
+// A duty found at level 1.5b goes straight to 2b with A = the chunk's value
+// (the only bad member's product IS the chunk's).
+
+// A failed duty with several candidates goes to level 2b with its A (every
+// lane of the quad stores its part; the lead takes the list slot).
+__device__ __forceinline__ void push_ident(const DevBatch& B, uint32_t d, const Fp4& A, bool lead) {
+  uint32_t slot = 0;
+  if (lead) {
+    slot = atomicAdd(&B.counters[CNT_DUTIES], 1u);
+    B.id_list[slot] = d;
+  }
+  slot = (uint32_t)__shfl((int)slot, (int)(threadIdx.x & ~3u));
+  quad_store(B.id_fe + (size_t)3 * QUAD_WORDS * slot, A);
+}
+// A duty known to be bad: one candidate -> that partial is invalid (the check
+// was its own, scaled by r != 0); several -> level 2b.
+__device__ __forceinline__ void resolve_bad_duty(const DevBatch& B, uint32_t d, const Fp4& A, bool lead) {
+  if (rlc_candidates(B, d) > 1) push_ident(B, d, A, lead);
+  else if (lead) rlc_mark(B, d, TBG_PS_INVALID);
+}
+
 // Level 1.5 check: one quad per listed chunk: its stored P-pair product
 // times the Miller loop of S_c, one final exponentiation.  Pass -> the
-// chunk's duties are valid; fail -> its duties go to level 2.
+// chunk's duties are valid; fail -> a lone duty is resolved at once, several
+// go to level 1.5b with the chunk's value (a degenerate S_c: level 3).
 __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t k = t >> 2;
@@ -284,101 +330,135 @@ __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C, nq = nch + 1;
   const uint32_t entry = B.chunk_list[k], qc = entry & ~CHUNK_DEGENERATE, g = qc / nch, c = qc % nch;
   const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
-  bool ok = false;
-  if (!(entry & CHUNK_DEGENERATE)) {
-    const uint32_t* ls = B.chunk_lines + (size_t)LINES_WORDS * k;
-    Fp4 f = quad_one();
-    int idx = 0;
-    for (int b = 62; b >= 0; --b) {
-      if (b != 62) f = quad_sqr(f);
-      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-      for (int s = 0; s < steps; ++s, ++idx) f = quad_line_folded(f, ls, idx);
-    }
-    f = quad_mul(f, quad_load(B.chunk_f + (size_t)3 * QUAD_WORDS * (g * nq + c)));
-    f = quad_final_exp(quad_conj(f));
-    ok = quad_is_one(f);
+  if (entry & CHUNK_DEGENERATE) {
+    if (lead)
+      for (uint32_t d = d0; d < d1; ++d)
+        if (rlc_combinable(B, d)) rlc_push_partials(B, d);
+    return;
   }
-  if (!lead) return;
-  uint32_t n = 0;
-  for (uint32_t d = d0; d < d1; ++d) n += rlc_combinable(B, d) ? 1u : 0u;
-  for (uint32_t d = d0; d < d1; ++d) {
-    if (!rlc_combinable(B, d)) continue;
-    if (ok) rlc_mark(B, d, TBG_PS_VALID);
-    else B.dv_list[atomicAdd(&B.counters[CNT_DUTIES], 1u)] = d;  // (a lone duty: level 2 repeats the
-                                                                    // check but keeps its value for 2b)
-  }
-}
-
-// Level 2 lines: one thread per listed duty.
-__global__ void TBG_LAUNCH k_rlc_duty_lines(DevBatch B) {
-  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= B.counters[CNT_DUTIES]) return;
-  uint32_t d = B.dv_list[k];
-  G2A Sa;
-  if (!jac_to_aff(B.dv_s[d], Sa)) return;  // excluded in k_rlc_duty_sum
-  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.dv_lines + (size_t)LINES_WORDS * k);
-}
-
-__device__ __forceinline__ uint32_t rlc_candidates(const DevBatch& B, uint32_t d) {
-  uint32_t n = 0;
-  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) n += rlc_candidate(B, i) ? 1u : 0u;
-  return n;
-}
-
-// Level 2 check: one quad per listed duty.  A failed duty with one candidate
-// is decided (the check is that partial's own, scaled by r != 0); a failed
-// duty with several keeps its final-exponentiated value A_d for level 2b.
-__global__ void TBG_LAUNCH k_rlc_check_duties(DevBatch B) {
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = t >> 2;
-  if (k >= B.counters[CNT_DUTIES]) return;
-  const bool lead = (t & 3) == 0;
-  uint32_t d = B.dv_list[k];
-  const G1A& P = B.dv_p[d];
-  Fp nx = fp_reduce(fp_neg(P.x));
-  const uint32_t* ls = B.dv_lines + (size_t)LINES_WORDS * k;
-  const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d];
+  const uint32_t* ls = B.chunk_lines + (size_t)LINES_WORDS * k;
   Fp4 f = quad_one();
   int idx = 0;
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = quad_sqr(f);
     int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-    for (int s = 0; s < steps; ++s, ++idx) {
-      f = quad_line_folded(f, ls, idx);
-      f = quad_line_at(f, lh, idx, nx, P.y);
-    }
+    for (int s = 0; s < steps; ++s, ++idx) f = quad_line_folded(f, ls, idx);
   }
+  f = quad_mul(f, quad_load(B.chunk_f + (size_t)3 * QUAD_WORDS * (g * nq + c)));
   f = quad_final_exp(quad_conj(f));
-  bool ok = quad_is_one(f);
-  if (!ok && rlc_candidates(B, d) > 1) {
-    quad_store(B.dv_fe + (size_t)3 * QUAD_WORDS * k, f);
-    if (lead) B.id_list[atomicAdd(&B.counters[CNT_IDENT], 1u)] = k;
+  if (quad_is_one(f)) {
+    if (lead)
+      for (uint32_t d = d0; d < d1; ++d)
+        if (rlc_combinable(B, d)) rlc_mark(B, d, TBG_PS_VALID);
     return;
   }
-  if (lead) rlc_mark(B, d, ok ? TBG_PS_VALID : TBG_PS_INVALID);
+  uint32_t n = 0, lone = d0;
+  for (uint32_t d = d0; d < d1; ++d)
+    if (rlc_combinable(B, d)) { ++n; lone = d; }
+  if (n == 1) {
+    resolve_bad_duty(B, lone, f, lead);
+    return;
+  }
+  quad_store(B.chunk_fe + (size_t)3 * QUAD_WORDS * k, f);
+  if (lead) B.cid_list[atomicAdd(&B.counters[CNT_CID], 1u)] = k;
 }
 
-// Level 2b: find the invalid partial of a failed duty with one extra check
-// instead of one per partial (the exponent test of Lee, Cheon and Hong,
-// "Finding invalid signatures in pairing-based batches").  With
-// eps_i = e(pk_i, H(m)) e(-g1, s_i) (1 iff partial i is valid) and weights
-// w_i = 1..n over the candidates,
-//   A_d  = prod_i eps_i^(r_i)        (level 2's value, kept in dv_fe),
-//   A'_d = prod_i eps_i^(w_i r_i)    (this level: P' = sum w_i r_i pk_i, S' = sum w_i r_i s_i).
-// If exactly partial b is invalid, A'_d = A_d^(w_b): b is found, the others are
-// valid.  A match for any w with two or more invalid partials needs the
-// secret r_i to satisfy a fixed linear relation (probability n 2^-64, the RLC
-// bound); no match sends the duty's candidates to level 3.
+// Level 1.5b lines, one thread per entry: S'_c = sum_d w_d S_d (suffix sums)
+// and the points w_d P_d, stored as (-x, y) for the line evaluations.
 constexpr uint32_t ID_DEGENERATE = 0x80000000u;
+__global__ void TBG_LAUNCH k_rlc_cident_lines(DevBatch B) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B.counters[CNT_CID]) return;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C;
+  const uint32_t k = B.cid_list[j], qc = B.chunk_list[k], g = qc / nch, c = qc % nch;
+  const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
+  G2J T = jac_inf<Fp2>(), U = jac_inf<Fp2>();
+  for (uint32_t d = d1; d-- > d0;) {
+    if (!rlc_combinable(B, d)) continue;
+    T = jac_add(T, B.dv_s[d]);
+    U = jac_add(U, T);
+  }
+  G2A Sa;
+  if (!jac_to_aff(U, Sa)) {
+    B.cid_list[j] = k | ID_DEGENERATE;
+    return;
+  }
+  uint32_t w = 0;
+  for (uint32_t d = d0; d < d1; ++d) {
+    if (!rlc_combinable(B, d)) continue;
+    ++w;
+    G1A wp = B.dv_p[d];
+    if (w > 1) jac_to_aff(jac_mul_u64(jac_from_aff(wp), w), wp);  // w < r: never the identity
+    wp.x = fp_reduce(fp_neg(wp.x));
+    B.cid_p[(size_t)C * j + (w - 1)] = wp;
+  }
+  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.cid_lines + (size_t)LINES_WORDS * j);
+}
 
-// Lines of S' and affine P', one thread per level-2b entry.  w_i = 1..n is the
-// candidate's rank from the duty's start, summed as suffix sums from its end
-// (U = sum_j T_j, T_j = sum of the last j candidates: two additions each).
+// Level 1.5b check: one quad per entry computes A'_c over the chunk's duties
+// and tests A_c^w == A'_c.  Found -> the other duties are valid and duty w
+// is resolved with A = A_c; not found (two or more bad duties, rare) -> the
+// chunk's candidates go to level 3.
+__global__ void TBG_LAUNCH k_rlc_cident_check(DevBatch B) {
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t j = t >> 2;
+  if (j >= B.counters[CNT_CID]) return;
+  const bool lead = (t & 3) == 0;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C;
+  const uint32_t entry = B.cid_list[j], k = entry & ~ID_DEGENERATE;
+  const uint32_t qc = B.chunk_list[k], g = qc / nch, c = qc % nch;
+  const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
+  uint32_t found = 0, n = 0;
+  for (uint32_t d = d0; d < d1; ++d) n += rlc_combinable(B, d) ? 1u : 0u;
+  const Fp4 A = quad_load(B.chunk_fe + (size_t)3 * QUAD_WORDS * k);
+  if (!(entry & ID_DEGENERATE)) {
+    const uint32_t* ls = B.cid_lines + (size_t)LINES_WORDS * j;
+    const G1A* wp = B.cid_p + (size_t)C * j;
+    Fp4 f = quad_one();
+    int idx = 0;
+    for (int b = 62; b >= 0; --b) {
+      if (b != 62) f = quad_sqr(f);
+      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+      for (int s = 0; s < steps; ++s, ++idx) {
+        f = quad_line_folded(f, ls, idx);
+        uint32_t r = 0;
+        for (uint32_t d = d0; d < d1; ++d) {
+          if (!rlc_combinable(B, d)) continue;
+          const G1A& P = wp[r++];
+          f = quad_line_at(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
+        }
+      }
+    }
+    const Fp4 inv_a2 = quad_final_exp(f);  // (A'_c)^-1: the conjugate is the inverse in GT
+    Fp4 Aw = A;
+    for (uint32_t w = 1; w <= n; ++w) {  // quad-uniform: quad_is_one agrees on all lanes
+      if (quad_is_one(quad_mul(Aw, inv_a2))) {
+        found = w;
+        break;
+      }
+      Aw = quad_mul(Aw, A);
+    }
+  }
+  uint32_t w = 0, bad = d0;
+  for (uint32_t d = d0; d < d1; ++d) {
+    if (!rlc_combinable(B, d)) continue;
+    if (++w == found) bad = d;
+    else if (lead) {
+      if (found) rlc_mark(B, d, TBG_PS_VALID);
+      else rlc_push_partials(B, d);
+    }
+  }
+  if (found) resolve_bad_duty(B, bad, A, lead);
+}
+
+// Level 2b lines, one thread per entry: P' = sum w_i r_i pk_i (affine) and
+// the lines of S' = sum w_i r_i s_i, w_i = 1..n the candidate's rank from the
+// duty's start (suffix sums from its end: two additions per candidate).
 __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= B.counters[CNT_IDENT]) return;
-  const uint32_t e = B.id_list[k], d = B.dv_list[e];
+  if (k >= B.counters[CNT_DUTIES]) return;
+  const uint32_t d = B.id_list[k];
   G1J Tp = jac_inf<Fp>(), Up = jac_inf<Fp>();
   G2J Ts = jac_inf<Fp2>(), Us = jac_inf<Fp2>();
   for (uint32_t i = B.duty_first[d + 1]; i-- > B.duty_first[d];) {
@@ -391,7 +471,7 @@ __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
   G1A Pa;
   G2A Sa;
   if (!jac_to_aff(Up, Pa) || !jac_to_aff(Us, Sa)) {
-    B.id_list[k] = e | ID_DEGENERATE;
+    B.id_list[k] = d | ID_DEGENERATE;
     return;
   }
   B.id_p[k] = Pa;
@@ -400,13 +480,14 @@ __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
 }
 
 // Level 2b check: one quad per entry computes A'_d and tests A_d^w == A'_d.
+// Found -> partial w invalid, the others valid; not found -> level 3.
 __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t k = t >> 2;
-  if (k >= B.counters[CNT_IDENT]) return;
+  if (k >= B.counters[CNT_DUTIES]) return;
   const bool lead = (t & 3) == 0;
-  const uint32_t entry = B.id_list[k], e = entry & ~ID_DEGENERATE, d = B.dv_list[e];
-  uint32_t found = 0;  // weight of the one invalid candidate; 0 = not identified
+  const uint32_t entry = B.id_list[k], d = entry & ~ID_DEGENERATE;
+  uint32_t found = 0;
   if (!(entry & ID_DEGENERATE)) {
     const G1A P = B.id_p[k];
     Fp nx = fp_reduce(fp_neg(P.x));
@@ -422,11 +503,11 @@ __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
         f = quad_line_at(f, lh, idx, nx, P.y);
       }
     }
-    const Fp4 inv_a2 = quad_final_exp(f);  // (A'_d)^-1: the conjugate is the inverse in GT
-    const Fp4 A = quad_load(B.dv_fe + (size_t)3 * QUAD_WORDS * e);
+    const Fp4 inv_a2 = quad_final_exp(f);
+    const Fp4 A = quad_load(B.id_fe + (size_t)3 * QUAD_WORDS * k);
     const uint32_t n = rlc_candidates(B, d);
     Fp4 Aw = A;
-    for (uint32_t w = 1; w <= n; ++w) {  // quad-uniform: quad_is_one agrees on all lanes
+    for (uint32_t w = 1; w <= n; ++w) {
       if (quad_is_one(quad_mul(Aw, inv_a2))) {
         found = w;
         break;
@@ -523,8 +604,8 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
     if (B.rlc_group > 1) {
       TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_check_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
-      TBG_KLAUNCH(k_rlc_duty_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
-      TBG_KLAUNCH(k_rlc_check_duties, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_cident_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_cident_check, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_ident_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_ident_check, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
     }

@@ -428,10 +428,12 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_gst = sec(4ull * ng);
   size_t w_gl = sec(4ull * LINES_WORDS * ng);
   size_t w_cnt = sec(4ull * CNT_WORDS);
-  size_t w_dvl = sec(G > 1 ? 4ull * nd : 0);
-  size_t w_dvlines = sec(G > 1 ? 4ull * LINES_WORDS * nd : 0);
   size_t w_pl = sec(verify ? 4ull * np : 0);
   size_t w_dvfe = sec(G > 1 ? 4ull * 3 * 4 * NL * nd : 0);
+  size_t w_cfe = sec(G > 1 ? 4ull * 3 * 4 * NL * ng * nch : 0);
+  size_t w_cidl = sec(G > 1 ? 4ull * ng * nch : 0);
+  size_t w_cidp = sec(G > 1 ? sizeof(G1A) * (size_t)ng * nch * C : 0);
+  size_t w_cidlines = sec(G > 1 ? 4ull * LINES_WORDS * ng * nch : 0);
   size_t w_idl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_idp = sec(G > 1 ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_aacc = sec(op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
@@ -549,10 +551,12 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.grp_state = (int32_t*)(dw + w_gst);
   B.grp_lines = (uint32_t*)(dw + w_gl);
   B.counters = (uint32_t*)(dw + w_cnt);
-  B.dv_list = (uint32_t*)(dw + w_dvl);
-  B.dv_lines = (uint32_t*)(dw + w_dvlines);
   B.part_list = (uint32_t*)(dw + w_pl);
-  B.dv_fe = (uint32_t*)(dw + w_dvfe);
+  B.id_fe = (uint32_t*)(dw + w_dvfe);
+  B.chunk_fe = (uint32_t*)(dw + w_cfe);
+  B.cid_list = (uint32_t*)(dw + w_cidl);
+  B.cid_p = (G1A*)(dw + w_cidp);
+  B.cid_lines = (uint32_t*)(dw + w_cidlines);
   B.id_list = (uint32_t*)(dw + w_idl);
   B.id_p = (G1A*)(dw + w_idp);
   B.id_lines = B.sig_lines;  // nd <= np list positions; level 3 rewrites them after level 2b
@@ -834,6 +838,212 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
   if (hipStreamSynchronize(st) != hipSuccess) rc = TBG_E_DEVICE;
   hipFree(base);
   return rc;
+}
+
+// ---- plain sums and FastAggregateVerify (k_sum.hip) -----------------------
+// dkg/dkg.go:466-476 (AggregateSignatures / AggregatePublicKeys of the lock
+// hash), cluster/lock.go:155-177 (FastAggregateVerify over every pubshare).
+
+}  // extern "C"
+
+namespace {
+
+// One device allocation for a utility call, freed on scope exit.
+struct DevArena {
+  uint8_t* base = nullptr;
+  size_t o = 0;
+  ~DevArena() {
+    if (base) hipFree(base);
+  }
+  int alloc(size_t bytes) { return hipMalloc(&base, bytes ? bytes : 16) == hipSuccess ? TBG_OK : TBG_E_OOM; }
+  uint8_t* sec(size_t bytes) {
+    uint8_t* p = base + o;
+    o += align_up(bytes, 16);
+    return p;
+  }
+};
+
+bool offsets_ok(const uint32_t* off, uint32_t n_sets) {
+  if (!off || off[0] != 0) return false;
+  for (uint32_t s = 0; s < n_sets; ++s)
+    if (off[s + 1] < off[s]) return false;
+  return true;
+}
+
+// Host half of a sum plan and its device copy inside `a`.
+struct SumHost {
+  std::vector<uint32_t> chunk_first, chunk_set;
+  static size_t bytes(uint32_t n_sets, uint32_t n_chunks, size_t part_elem) {
+    return align_up(4ull * (n_sets + 1), 16) * 2 + align_up(4ull * n_chunks + 4, 16) +
+           align_up(part_elem * n_chunks + 16, 16) + align_up(4ull * n_sets + 4, 16);
+  }
+  SumHost(const uint32_t* off, uint32_t n_sets) {
+    const uint32_t ch = tbg::sum_chunk_size();
+    chunk_first.resize(n_sets + 1);
+    chunk_first[0] = 0;
+    for (uint32_t s = 0; s < n_sets; ++s) {
+      const uint32_t nc = (off[s + 1] - off[s] + ch - 1) / ch;
+      chunk_first[s + 1] = chunk_first[s] + nc;
+      for (uint32_t k = 0; k < nc; ++k) chunk_set.push_back(s);
+    }
+  }
+  uint32_t n_chunks() const { return chunk_first.back(); }
+  int upload(DevArena& a, const uint32_t* off, uint32_t n_sets, size_t part_elem, hipStream_t st, tbg::SumPlan& p) {
+    uint32_t* d_off = (uint32_t*)a.sec(4ull * (n_sets + 1));
+    uint32_t* d_cf = (uint32_t*)a.sec(4ull * (n_sets + 1));
+    uint32_t* d_cs = (uint32_t*)a.sec(4ull * n_chunks() + 4);
+    p.part = a.sec(part_elem * n_chunks() + 16);
+    p.set_bad = (int32_t*)a.sec(4ull * n_sets + 4);
+    p.n_sets = n_sets;
+    p.n_chunks = n_chunks();
+    p.off = d_off;
+    p.chunk_first = d_cf;
+    p.chunk_set = d_cs;
+    if (hipMemcpyAsync(d_off, off, 4ull * (n_sets + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_cf, chunk_first.data(), 4ull * (n_sets + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
+        (n_chunks() && hipMemcpyAsync(d_cs, chunk_set.data(), 4ull * n_chunks(), hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipMemsetAsync(p.set_bad, 0, 4ull * n_sets, st) != hipSuccess)
+      return TBG_E_DEVICE;
+    return TBG_OK;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int tbg_sum_pubkeys(tbg_ctx* c, const uint32_t* pubkey_ids, const uint32_t* off, uint32_t n_sets, uint8_t* out48,
+                    int32_t* status) {
+  if (!c || !n_sets || !out48 || !status || !offsets_ok(off, n_sets)) return TBG_E_INVALID_ARG;
+  const uint32_t ni = off[n_sets];
+  if (ni && !pubkey_ids) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  SumHost h(off, n_sets);
+  DevArena a;
+  int rc = a.alloc(SumHost::bytes(n_sets, h.n_chunks(), sizeof(G1J)) + align_up(4ull * ni + 4, 16) +
+                   align_up(48ull * n_sets, 16) + align_up(4ull * n_sets, 16));
+  if (rc != TBG_OK) return rc;
+  hipStream_t st = c->stream;
+  tbg::SumPlan p;
+  if ((rc = h.upload(a, off, n_sets, sizeof(G1J), st, p)) != TBG_OK) return rc;
+  uint32_t* d_ids = (uint32_t*)a.sec(4ull * ni + 4);
+  uint8_t* d_out = a.sec(48ull * n_sets);
+  int32_t* d_st = (int32_t*)a.sec(4ull * n_sets);
+  if (ni) HIP_TRY(hipMemcpyAsync(d_ids, pubkey_ids, 4ull * ni, hipMemcpyHostToDevice, st));
+  tbg::launch_sum_g1(c->d_pk, c->d_pk_status, c->n_pk, d_ids, p, d_out, d_st, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out48, d_out, 48ull * n_sets, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(status, d_st, 4ull * n_sets, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return TBG_OK;
+}
+
+int tbg_sum_sigs(tbg_ctx* c, const uint8_t* sigs96, const uint32_t* off, uint32_t n_sets, uint8_t* out96,
+                 int32_t* status, int32_t* sig_status) {
+  if (!c || !n_sets || !out96 || !status || !offsets_ok(off, n_sets)) return TBG_E_INVALID_ARG;
+  const uint32_t ni = off[n_sets];
+  if (ni && !sigs96) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  SumHost h(off, n_sets);
+  DevArena a;
+  int rc = a.alloc(SumHost::bytes(n_sets, h.n_chunks(), sizeof(G2J)) + align_up(96ull * ni + 4, 16) +
+                   align_up(4ull * ni + 4, 16) + align_up(96ull * n_sets, 16) + align_up(4ull * n_sets, 16));
+  if (rc != TBG_OK) return rc;
+  hipStream_t st = c->stream;
+  tbg::SumPlan p;
+  if ((rc = h.upload(a, off, n_sets, sizeof(G2J), st, p)) != TBG_OK) return rc;
+  uint8_t* d_sigs = a.sec(96ull * ni + 4);
+  int32_t* d_sst = (int32_t*)a.sec(4ull * ni + 4);
+  uint8_t* d_out = a.sec(96ull * n_sets);
+  int32_t* d_st = (int32_t*)a.sec(4ull * n_sets);
+  if (ni) HIP_TRY(hipMemcpyAsync(d_sigs, sigs96, 96ull * ni, hipMemcpyHostToDevice, st));
+  tbg::launch_sum_g2(d_sigs, p, d_out, d_st, d_sst, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out96, d_out, 96ull * n_sets, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(status, d_st, 4ull * n_sets, hipMemcpyDeviceToHost, st));
+  if (sig_status && ni) HIP_TRY(hipMemcpyAsync(sig_status, d_sst, 4ull * ni, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return TBG_OK;
+}
+
+int tbg_fast_aggregate_verify(tbg_ctx* c, const uint32_t* pubkey_ids, const uint32_t* key_off, uint32_t n_sets,
+                              const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* sigs96, int32_t* status) {
+  if (!c || !n_sets || !sigs96 || !status || !offsets_ok(key_off, n_sets) || !offsets_ok(msg_off, n_sets))
+    return TBG_E_INVALID_ARG;
+  const uint32_t nk = key_off[n_sets];
+  const size_t mb = msg_off[n_sets];
+  if ((nk && !pubkey_ids) || (mb && !msgs)) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  const uint32_t n = n_sets;
+  SumHost h(key_off, n);
+  std::vector<uint32_t> iota(n + 1);
+  for (uint32_t i = 0; i <= n; ++i) iota[i] = i;
+  const size_t lines = 4ull * LINES_WORDS * n;
+  DevArena a;
+  int rc = a.alloc(SumHost::bytes(n, h.n_chunks(), sizeof(G1J)) + align_up(4ull * nk + 4, 16) +
+                   align_up(48ull * n, 16) * 2 + align_up(sizeof(G1A) * n, 16) * 2 + align_up(4ull * n, 16) * 6 +
+                   align_up(mb + 1, 16) + align_up(4ull * (n + 1), 16) * 2 + align_up(96ull * n, 16) + align_up(n, 16) +
+                   align_up(sizeof(G2A) * n, 16) * 2 + align_up(sizeof(G2J) * n, 16) + 2 * align_up(lines, 16) +
+                   align_up(4ull * tbg::CNT_WORDS, 16));
+  if (rc != TBG_OK) return rc;
+  hipStream_t st = c->stream;
+  // 1. the key sums, compressed, then decoded into a table of their own
+  tbg::SumPlan p;
+  if ((rc = h.upload(a, key_off, n, sizeof(G1J), st, p)) != TBG_OK) return rc;
+  uint32_t* d_ids = (uint32_t*)a.sec(4ull * nk + 4);
+  uint8_t* d_pk48 = a.sec(48ull * n);
+  int32_t* d_kst = (int32_t*)a.sec(4ull * n);
+  G1A* t_pk = (G1A*)a.sec(sizeof(G1A) * n);
+  G1A* t_xpk = (G1A*)a.sec(sizeof(G1A) * n);
+  int32_t* t_pkst = (int32_t*)a.sec(4ull * n);
+  if (nk) HIP_TRY(hipMemcpyAsync(d_ids, pubkey_ids, 4ull * nk, hipMemcpyHostToDevice, st));
+  tbg::launch_sum_g1(c->d_pk, c->d_pk_status, c->n_pk, d_ids, p, d_pk48, d_kst, st);
+  tbg::launch_decode_pubkeys(d_pk48, n, t_pk, t_xpk, t_pkst, st);  // a failed / identity sum: not DEC_OK
+  // 2. one CoreVerify per set against that table (the per-item schedule)
+  DevBatch B;
+  memset(&B, 0, sizeof(B));
+  B.op = TBG_OP_VERIFY;
+  B.n_duties = B.n_partials = B.n_msgs = n;
+  uint8_t* d_msgs = a.sec(mb + 1);
+  uint32_t* d_moff = (uint32_t*)a.sec(4ull * (n + 1));
+  uint32_t* d_iota = (uint32_t*)a.sec(4ull * (n + 1));
+  uint8_t* d_sigs = a.sec(96ull * n);
+  uint8_t* d_idf = a.sec(n);
+  B.msgs = d_msgs;
+  B.msg_off = d_moff;
+  B.duty_msg = B.duty_first = B.partial_duty = B.pubkey_ids = d_iota;
+  B.duty_threshold = d_iota;  // unused by TBG_OP_VERIFY
+  B.sigs = d_sigs;
+  B.identifiers = d_idf;
+  B.sig_aff = (G2A*)a.sec(sizeof(G2A) * n);
+  B.h_aff = (G2A*)a.sec(sizeof(G2A) * n);
+  B.h_status = (int32_t*)a.sec(4ull * n);
+  B.h_jac = (G2J*)a.sec(sizeof(G2J) * n);
+  B.sig_lines = (uint32_t*)a.sec(lines);
+  B.h_lines = (uint32_t*)a.sec(lines);
+  B.counters = (uint32_t*)a.sec(4ull * tbg::CNT_WORDS);
+  B.part_list = (uint32_t*)a.sec(4ull * n);
+  B.partial_status = (int32_t*)a.sec(4ull * n);
+  B.duty_status = (int32_t*)a.sec(4ull * n);
+  B.rlc_group = 0;
+  if (mb) HIP_TRY(hipMemcpyAsync(d_msgs, msgs, mb, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(d_moff, msg_off, 4ull * (n + 1), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(d_iota, iota.data(), 4ull * (n + 1), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(d_sigs, sigs96, 96ull * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(d_idf, 0, n, st));
+  HIP_TRY(hipMemsetAsync(B.counters, 0, 4 * tbg::CNT_WORDS, st));
+  tbg::launch_decode_sigs(B, st);
+  tbg::launch_hash_msgs(B, st);
+  tbg::launch_h_lines(B, st);
+  tbg::launch_rlc_prepare(B, t_pk, t_xpk, t_pkst, n, st);
+  tbg::launch_rlc_check(B, t_pk, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(status, B.partial_status, 4ull * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return TBG_OK;
 }
 
 }  // extern "C"

@@ -69,11 +69,13 @@ struct DevBatch {
   int32_t* grp_state;     // [n_groups] GRP_*
   uint32_t* grp_lines;    // [n_groups][LINES_WORDS] lines of the group's S (-g1 folded in)
   uint32_t* counters;     // [CNT_*] work-list lengths
-  uint32_t* dv_list;      // [n_duties] level-2 duties
-  uint32_t* dv_lines;     // [n_duties][LINES_WORDS] lines of S_d, by level-2 list position
   uint32_t* part_list;    // [n_partials] level-3 partials (sig_lines by list position)
-  uint32_t* dv_fe;        // [n_duties][3][4 NL] final-exponentiated level-2 value of failed duties (by list position)
-  uint32_t* id_list;      // [n_duties] level-2b entries: level-2 list positions of failed multi-partial duties
+  uint32_t* chunk_fe;     // [n_groups * chunks][3][4 NL] final-exponentiated value of failed chunks (by list position)
+  uint32_t* cid_list;     // [n_groups * chunks] level-1.5b entries: chunk-list positions
+  G1A* cid_p;             // [n_groups * chunks][rlc_chunk] w_d P_d as (-x, y), by level-1.5b position
+  uint32_t* cid_lines;    // [n_groups * chunks][LINES_WORDS] lines of sum w_d S_d, by level-1.5b position
+  uint32_t* id_fe;        // [n_duties][3][4 NL] value A_d of each level-2b duty (by list position)
+  uint32_t* id_list;      // [n_duties] level-2b entries: failed duties with several candidates
   G1A* id_p;              // [n_duties] sum w_i r_i pk_i (affine), by level-2b position
   uint32_t* id_lines;     // lines of sum w_i r_i sig_i by level-2b position: aliases sig_lines,
                           // which level 3 only fills after level 2b has consumed them
@@ -88,7 +90,9 @@ struct DevBatch {
 
 enum RlcState : int32_t { RLC_NONE = 0, RLC_COMBINED = 1, RLC_EACH = 2 };
 enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3 };
-enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_IDENT = 4, CNT_WORDS = 5 };
+// CNT_DUTIES: level-2b duties (id_list), CNT_PARTIALS: level-3 partials, CNT_AGG: [1/D] duties,
+// CNT_CHUNKS: level-1.5 chunks, CNT_CID: level-1.5b chunks
+enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_CID = 4, CNT_WORDS = 5 };
 
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {
@@ -106,6 +110,21 @@ void debug_after_launch(const char* kernel, hipStream_t st);
   } while (0)
 
 // launchers (asynchronous on `st`)
+// Device arrays of one plain-sum call (k_sum.hip): n_sets sets of items,
+// summed in chunks of sum_chunk_size() items.
+struct SumPlan {
+  uint32_t n_sets, n_chunks;
+  const uint32_t* off;          // [n_sets + 1] item offsets of the sets
+  const uint32_t* chunk_first;  // [n_sets + 1] first chunk of each set
+  const uint32_t* chunk_set;    // [n_chunks] set of each chunk
+  void* part;                   // [n_chunks] G1J / G2J chunk sums
+  int32_t* set_bad;             // [n_sets] zeroed before the launch
+};
+uint32_t sum_chunk_size();
+void launch_sum_g1(const G1A* table, const int32_t* pk_status, uint32_t n_pk, const uint32_t* ids, const SumPlan& p,
+                   uint8_t* out48, int32_t* status, hipStream_t st);
+void launch_sum_g2(const uint8_t* sigs96, const SumPlan& p, uint8_t* out96, int32_t* status, int32_t* sig_status,
+                   hipStream_t st);
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st);
 void launch_decode_sigs(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);

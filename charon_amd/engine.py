@@ -233,6 +233,41 @@ class Engine:
         return out
 
 
+    # ---- plain sums / FastAggregateVerify (DKG, cluster lock) ----
+    def sum_pubkeys(self, pubkey_ids, off):
+        """Sums of resident keys per set -> (48-byte sums [n_sets, 48], status [n_sets])."""
+        ids, off = _u32(pubkey_ids), _u32(off)
+        n = len(off) - 1
+        out = np.zeros((n, 48), dtype=np.uint8)
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self._lib.tbg_sum_pubkeys(self._h, _ptr(ids), _ptr(off), n, _ptr(out), _ptr(st)),
+                    "tbg_sum_pubkeys")
+        return out, st
+
+    def sum_sigs(self, sigs, off):
+        """Decoded sums of 96-byte signatures per set -> (sums [n_sets, 96],
+        status [n_sets], per-signature decode status)."""
+        a, off = _u8(sigs, 96), _u32(off)
+        n = len(off) - 1
+        out = np.zeros((n, 96), dtype=np.uint8)
+        st = np.zeros(n, dtype=np.int32)
+        sst = np.zeros(max(1, a.shape[0]), dtype=np.int32)
+        self._check(self._lib.tbg_sum_sigs(self._h, _ptr(a), _ptr(off), n, _ptr(out), _ptr(st), _ptr(sst)),
+                    "tbg_sum_sigs")
+        return out, st, sst[:a.shape[0]]
+
+    def fast_aggregate_verify(self, pubkey_ids, key_off, msgs, sigs):
+        """Per set: CoreVerify(sum of its resident keys, msg, sig) -> status [n_sets]."""
+        ids, koff = _u32(pubkey_ids), _u32(key_off)
+        data, moff = msgs if isinstance(msgs, tuple) else pack_messages(msgs)
+        data, moff, a = _u8(data), _u32(moff), _u8(sigs, 96)
+        n = len(koff) - 1
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self._lib.tbg_fast_aggregate_verify(self._h, _ptr(ids), _ptr(koff), n, _ptr(data), _ptr(moff),
+                                                        _ptr(a), _ptr(st)), "tbg_fast_aggregate_verify")
+        return st
+
+
 class MultiEngine:
     """One process, several GPUs (tbg_multi_*): batches are cut into
     contiguous duty ranges, one per context, submitted concurrently and

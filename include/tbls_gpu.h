@@ -170,9 +170,32 @@ int tbg_replay_multi(tbg_ctx* ctx, const tbg_ticket* tickets, uint32_t n_tickets
 int tbg_replay_plan(tbg_ctx* ctx, const tbg_ticket* tickets, const uint32_t* n_parts, uint32_t n_launches, float* ms8);
 int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
 /* Verification work of a collected batch's last run: out4 = [level-1 groups,
- * duties re-checked alone (level 2), partials checked one by one (level 3),
- * duties per group (0 = TBG_VERIFY_EACH)]. */
+ * failed duties searched for their invalid partial (level 2b), partials
+ * checked one by one (level 3), duties per group (0 = TBG_VERIFY_EACH)]. */
 int tbg_fetch_stats(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out4);
+
+/* Plain BLS aggregation (every coefficient 1) for the DKG / cluster-lock
+ * multi-signatures: AggregatePublicKeys / AggregateSignatures of
+ * aggLockHashSig (reference dkg/dkg.go:466-476) and FastAggregateVerify of
+ * Lock.VerifySignatures (cluster/lock.go:155-177).  Set k covers items
+ * [off[k], off[k+1]); off[0] = 0.
+ * tbg_sum_pubkeys: sum of resident public keys (ids from tbg_load_pubkeys);
+ *   out48[k] the compressed sum, status[k] TBG_DS_OK, TBG_DS_AGG_IDENTITY
+ *   (empty set or identity sum; out48 = the identity encoding) or
+ *   TBG_DS_DECODE (an unknown id or a key that failed to decode; out48 zero).
+ * tbg_sum_sigs: decode (flags, field, curve, subgroup) and sum 96-byte
+ *   signatures; status as above (the identity encoding decodes and adds
+ *   nothing); sig_status (optional) per signature: TBG_PS_NOT_VERIFIED, or
+ *   its decode code (TBG_PS_ERR_IDENTITY for the identity).
+ * tbg_fast_aggregate_verify: per set, CoreVerify(sum of its keys, msg k,
+ *   sig k) on the GPU; status[k] TBG_PS_VALID / TBG_PS_INVALID / a signature
+ *   decode code / TBG_PS_ERR_PUBKEY (the key sum failed or is the identity). */
+int tbg_sum_pubkeys(tbg_ctx* ctx, const uint32_t* pubkey_ids, const uint32_t* off, uint32_t n_sets, uint8_t* out48,
+                    int32_t* status);
+int tbg_sum_sigs(tbg_ctx* ctx, const uint8_t* sigs96, const uint32_t* off, uint32_t n_sets, uint8_t* out96,
+                 int32_t* status, int32_t* sig_status);
+int tbg_fast_aggregate_verify(tbg_ctx* ctx, const uint32_t* pubkey_ids, const uint32_t* key_off, uint32_t n_sets,
+                              const uint8_t* msgs, const uint32_t* msg_off, const uint8_t* sigs96, int32_t* status);
 
 /* Test-vector / benchmark-input generation on the GPU (not on the hot path):
  * tbls.Sign / PartialSign (reference tbls/tss.go:200-217) and

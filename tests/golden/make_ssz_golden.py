@@ -52,6 +52,10 @@ def main():
             "pubkey": "86966350b672bd502bfbdb37a6ea8a7392e8fb7f5ebb5c5e2055f4ee168ebfab0fef63084f28c9f62c3ba71f825e527e",
             "root": "2c231b16a80337212ab1decde301bdb4383e74c0bf2f3439cc82542bf0f90fdd",
             "domain_type": "00000001", "fork_version": "00001020",
+            # the signer is the secret share of signing_test.go:40 (its public
+            # share), not the DV key inside the message
+            "signer_secret": "345768c0245f1dc702df9e50e811002f61ebb2680b3d5931527ef59f96cbaf9b",
+            "signer_pubkey": "9305c3b8cf2f4ee9c636b2e5bd60b730e4816840f01683bdcb75352451e553839c9173cd4212c08947443692dc48eaf7",
             "signature": "b101da0fc08addcc5d010ee569f6bbbdca049a5cb27efad231565bff2e3af504ec2bb87b11ed22843e9c1094f"
                          "1dfe51a0b2a5ad1808df18530a2f59f004032dbf6281ecf0fc3df86d032da5b9d32a3d282c05923de491381f"
                          "8f28c2863a00180",

@@ -29,7 +29,8 @@ def test_header_declares_the_boundary():
                  "tbg_replay", "tbg_replay_multi", "tbg_fetch", "tbg_strerror", "tbg_sign", "tbg_sk_to_pk",
                  "tbg_poll", "tbg_multi_init", "tbg_multi_submit", "tbg_multi_collect", "tbg_multi_load_pubkeys",
                  "tbg_multi_context", "tbg_multi_layout", "tbg_ssz_roots", "tbg_signing_roots",
-                 "tbg_compute_domain", "tbg_ssz_size"]:
+                 "tbg_compute_domain", "tbg_ssz_size", "tbg_sum_pubkeys", "tbg_sum_sigs",
+                 "tbg_fast_aggregate_verify"]:
         assert must in names
 
 

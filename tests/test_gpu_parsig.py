@@ -165,7 +165,7 @@ def test_reference_signed_objects_verify_through_native_roots(engine):
     rspec = signing.Spec(forks=[(0, H(r["fork_version"]))])
     rroots = signing.message_signing_roots(rspec, signing.DOMAIN_APPLICATION_BUILDER, [0, 0], [reg, bad_reg])
     for rr in rroots:
-        items.append((tbls.PublicKey(H(r["pubkey"])), rr, tbls.Signature(H(r["signature"]))))
+        items.append((tbls.PublicKey(H(r["signer_pubkey"])), rr, tbls.Signature(H(r["signature"]))))
     got = tbls.verify_batch(items, engine)
     n = len(deps)
     assert got == [True, False] + [True] * n + [False] * n + [True, False]

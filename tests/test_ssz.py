@@ -64,6 +64,9 @@ def test_oracle_reference_registration():
     v = GOLD["validator_registration"]
     root = so.validator_registration_root(H(v["fee_recipient"]), v["gas_limit"], v["timestamp"], H(v["pubkey"]))
     assert root.hex() == v["root"]
+    from oracle import bls12_381 as bls
+    from oracle import tbls_oracle as tb
+    assert bls.g1_compress(tb.sk_to_pk(int(v["signer_secret"], 16))).hex() == v["signer_pubkey"]
 
 
 # ------------------------------------------------------------ native parity
