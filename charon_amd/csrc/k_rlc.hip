@@ -284,6 +284,20 @@ __device__ __forceinline__ uint32_t rlc_candidates(const DevBatch& B, uint32_t d
   return n;
 }
 
+// The fallback checks run their Miller loops and final exponentiations with
+// the squarings / line products inline (no scratch-stack call per step), as
+// the level-1 kernels do; TBG_FALLBACK_INL=0 builds the out-of-line form (A/B).
+#ifndef TBG_FALLBACK_INL
+#define TBG_FALLBACK_INL 1
+#endif
+#if TBG_FALLBACK_INL
+#define FB_SQR quad_sqr_in
+#define FB_FE quad_final_exp_in
+#else
+#define FB_SQR quad_sqr
+#define FB_FE quad_final_exp
+#endif
+
 // ---------------------------------------------------------- identification
 // The exponent test (Lee, Cheon and Hong, "Finding invalid signatures in
 // pairing-based batches") finds the one bad member of a failed product with
@@ -340,12 +354,12 @@ __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
   Fp4 f = quad_one();
   int idx = 0;
   for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = quad_sqr(f);
+    if (b != 62) f = FB_SQR(f);
     int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-    for (int s = 0; s < steps; ++s, ++idx) f = quad_line_folded(f, ls, idx);
+    for (int s = 0; s < steps; ++s, ++idx) f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
   }
   f = quad_mul(f, quad_load(B.chunk_f + (size_t)3 * QUAD_WORDS * (g * nq + c)));
-  f = quad_final_exp(quad_conj(f));
+  f = FB_FE(quad_conj(f));
   if (quad_is_one(f)) {
     if (lead)
       for (uint32_t d = d0; d < d1; ++d)
@@ -418,19 +432,19 @@ __global__ void TBG_LAUNCH k_rlc_cident_check(DevBatch B) {
     Fp4 f = quad_one();
     int idx = 0;
     for (int b = 62; b >= 0; --b) {
-      if (b != 62) f = quad_sqr(f);
+      if (b != 62) f = FB_SQR(f);
       int steps = ((X_ABS >> b) & 1) ? 2 : 1;
       for (int s = 0; s < steps; ++s, ++idx) {
-        f = quad_line_folded(f, ls, idx);
+        f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
         uint32_t r = 0;
         for (uint32_t d = d0; d < d1; ++d) {
           if (!rlc_combinable(B, d)) continue;
           const G1A& P = wp[r++];
-          f = quad_line_at(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
+          f = quad_line_at<TBG_FALLBACK_INL>(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
         }
       }
     }
-    const Fp4 inv_a2 = quad_final_exp(f);  // (A'_c)^-1: the conjugate is the inverse in GT
+    const Fp4 inv_a2 = FB_FE(f);  // (A'_c)^-1: the conjugate is the inverse in GT
     Fp4 Aw = A;
     for (uint32_t w = 1; w <= n; ++w) {  // quad-uniform: quad_is_one agrees on all lanes
       if (quad_is_one(quad_mul(Aw, inv_a2))) {
@@ -496,14 +510,14 @@ __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
     Fp4 f = quad_one();
     int idx = 0;
     for (int b = 62; b >= 0; --b) {
-      if (b != 62) f = quad_sqr(f);
+      if (b != 62) f = FB_SQR(f);
       int steps = ((X_ABS >> b) & 1) ? 2 : 1;
       for (int s = 0; s < steps; ++s, ++idx) {
-        f = quad_line_folded(f, ls, idx);
-        f = quad_line_at(f, lh, idx, nx, P.y);
+        f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
+        f = quad_line_at<TBG_FALLBACK_INL>(f, lh, idx, nx, P.y);
       }
     }
-    const Fp4 inv_a2 = quad_final_exp(f);
+    const Fp4 inv_a2 = FB_FE(f);
     const Fp4 A = quad_load(B.id_fe + (size_t)3 * QUAD_WORDS * k);
     const uint32_t n = rlc_candidates(B, d);
     Fp4 Aw = A;
@@ -568,14 +582,14 @@ __global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   Fp4 f = quad_one();
   int idx = 0;
   for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = quad_sqr(f);
+    if (b != 62) f = FB_SQR(f);
     int steps = ((X_ABS >> b) & 1) ? 2 : 1;
     for (int s = 0; s < steps; ++s, ++idx) {
-      f = quad_line_folded(f, ls, idx);
-      f = quad_line_at(f, lh, idx, nx, pk.y);
+      f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
+      f = quad_line_at<TBG_FALLBACK_INL>(f, lh, idx, nx, pk.y);
     }
   }
-  f = quad_final_exp(quad_conj(f));
+  f = FB_FE(quad_conj(f));
   bool ok = quad_is_one(f);
   if (lead) B.partial_status[i] = ok ? TBG_PS_VALID : TBG_PS_INVALID;
 }
