@@ -91,6 +91,8 @@ struct tbg_ctx {
   // exponentiations and Fp12 squarings per duty.
   uint32_t rlc_group = 16;  // 0 = per-partial checks (TBG_VERIFY_EACH)
   uint32_t rlc_chunk = 4;
+  bool rlc_auto = false;     // rlc_group follows the observed invalid share (tbg_config.rlc_group = 0)
+  double invalid_ema = 0.0;  // exponential average of the invalid share of collected verified partials
   uint64_t rlc_seed = 0;   // 0 = OS randomness per batch
   uint64_t seed_ctr = 0;
 };
@@ -159,6 +161,7 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   if (cfg && cfg->verify_mode == TBG_VERIFY_EACH) c->rlc_group = 0;
   else if (cfg && cfg->verify_mode != TBG_VERIFY_RLC) { delete c; return TBG_E_INVALID_ARG; }
   else if (cfg && cfg->rlc_group) c->rlc_group = cfg->rlc_group;
+  else c->rlc_auto = true;
   if (cfg && cfg->rlc_chunk) c->rlc_chunk = cfg->rlc_chunk;
   if (c->rlc_group > 4096 || c->rlc_chunk > 4096) { delete c; return TBG_E_INVALID_ARG; }
   c->rlc_seed = cfg ? cfg->rlc_seed : 0;
@@ -413,6 +416,8 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_lam = sec(32ull * np);
   size_t w_sl = sec(verify ? 4ull * LINES_WORDS * np : 0);
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
+  if (c->rlc_auto)
+    c->rlc_group = c->invalid_ema < TBG_RLC_AUTO_TO8 ? 16 : c->invalid_ema < TBG_RLC_AUTO_TO4 ? 8 : 4;
   const uint32_t G = verify ? c->rlc_group : 0;
   const uint32_t ng = G ? (nd + G - 1) / G : 0;
   const uint32_t C = c->rlc_chunk < G ? c->rlc_chunk : (G ? G : 1);
@@ -649,6 +654,12 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     return TBG_E_DEVICE;
   }
   copy_part(s, *q, pst, dst, agg);
+  if (c->rlc_auto && s->op != TBG_OP_AGGREGATE && q->np) {  // the adaptive group size's input
+    const int32_t* st = (const int32_t*)s->h_out;  // partial statuses lead the output region
+    uint32_t bad = 0;
+    for (uint32_t i = 0; i < q->np; ++i) bad += st[q->p0 + i] == TBG_PS_INVALID ? 1u : 0u;
+    c->invalid_ema = 0.5 * c->invalid_ema + 0.5 * (double)bad / q->np;
+  }
   chain_times(s->ev, s->ms);
   memcpy(c->last_ms, s->ms, sizeof(c->last_ms));
   part_done(s, q);

@@ -31,7 +31,8 @@ SCHEDULES = {
     "each": dict(verify_mode=1),
     # random linear combinations: one duty per group (levels 1 -> 3)
     "rlc1": dict(verify_mode=0, rlc_group=1, rlc_seed=0x5EED),
-    # the default: 16 duties per group, 4 per Miller quad, fresh OS randomness per batch
+    # the default: adaptive group size (16 while clean, 8 / 4 after invalid
+    # batches), 4 duties per Miller quad, fresh OS randomness per batch
     "rlc16": dict(verify_mode=0),
     # the previous default: 8 duties per group, 2 per quad
     "rlc8c2": dict(verify_mode=0, rlc_group=8, rlc_chunk=2, rlc_seed=0x8C2),
@@ -246,3 +247,26 @@ def test_rlc_cancelling_errors_across_duties_are_rejected(engine):
         assert bad[d] not in signers, d
         assert len(signers) >= v["tss"]["threshold"]
         assert sig.raw.hex() == v["expect"]["group_sig"]
+
+
+def test_adaptive_group_size_follows_invalid_share():
+    """tbg_config.rlc_group = 0: 16 duties per group while the collected
+    batches are clean, smaller groups once they carry invalid partials, and
+    back to 16 after clean ones; verdicts are exact throughout."""
+    from charon_amd import engine as eng
+    e = eng.Engine(0)
+    try:
+        def run(seed, inject):
+            b = _make_cluster_batch(e, 400, 3, 4, seed=seed, inject=inject)
+            t = e.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
+                         duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+            res = e.collect(t)
+            assert np.array_equal(res.partial_status == eng.PS_VALID, ~b.injected)
+            return e.stats(t)["group_size"]
+        assert run(31, 0.0) == 16
+        run(32, 0.05)
+        assert run(33, 0.05) in (4, 8)
+        sizes = [run(34 + k, 0.0) for k in range(8)]
+        assert sizes[-1] == 16
+    finally:
+        e.close()
