@@ -1,0 +1,49 @@
+// Miller lines of affine G2 points with the -g1 factor folded in (the S side
+// of every RLC product check), one lane PAIR per point with the Fp2
+// coordinates split over the pair (bls_pair.h, two waves per SIMD).  The
+// producers in k_rlc.hip form the sums and their affine points in
+// DevBatch::pend_pts (one inversion per lane); a single lane computing the 68
+// lines of a point was the latency of the group-lines and fallback-lines
+// kernels (157 waves for a 10k-DV batch's 625 groups).
+#ifndef TBG_SCHED_FENCE
+#define TBG_SCHED_FENCE 1  // products in program order: fits the pair kernel in 256 VGPRs (bls_field.h)
+#endif
+#include "tbls_launch.h"
+#include "bls_lines.h"
+#include "bls_pair.h"
+
+namespace tbg {
+
+template <int KIND>
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
+  const uint32_t k = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
+  uint32_t* out;
+  if (KIND == FOLD_GROUPS) {
+    if (k >= (B.n_duties + B.rlc_group - 1) / B.rlc_group || B.grp_state[k] != GRP_LINES) return;
+    out = B.grp_lines;
+  } else if (KIND == FOLD_CHUNKS) {
+    if (k >= B.counters[CNT_CHUNKS] || (B.chunk_list[k] & CHUNK_DEGENERATE)) return;
+    out = B.chunk_lines;
+  } else if (KIND == FOLD_CID) {
+    if (k >= B.counters[CNT_CID] || (B.cid_list[k] & ID_DEGENERATE)) return;
+    out = B.cid_lines;
+  } else {
+    if (k >= B.counters[CNT_DUTIES] || (B.id_list[k] & ID_DEGENERATE)) return;
+    out = B.id_lines;
+  }
+  const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  px_g2_lines(px_load(B.pend_pts[k]), nx, fp_from_const(G1_NEG_Y), out + (size_t)LINES_WORDS * k);
+}
+
+void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStream_t st) {
+  if (!max_entries) return;
+  const dim3 grid = grid_for(2 * max_entries);
+  switch (kind) {
+    case FOLD_GROUPS: TBG_KLAUNCH(k_lines_fold<FOLD_GROUPS>, grid, dim3(kBlock), st, B); break;
+    case FOLD_CHUNKS: TBG_KLAUNCH(k_lines_fold<FOLD_CHUNKS>, grid, dim3(kBlock), st, B); break;
+    case FOLD_CID: TBG_KLAUNCH(k_lines_fold<FOLD_CID>, grid, dim3(kBlock), st, B); break;
+    default: TBG_KLAUNCH(k_lines_fold<FOLD_IDENT>, grid, dim3(kBlock), st, B); break;
+  }
+}
+
+}  // namespace tbg

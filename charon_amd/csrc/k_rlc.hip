@@ -80,7 +80,8 @@ __global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B) {
   B.dv_state[d] = RLC_COMBINED;
 }
 
-// One thread per group: S = sum of the group's S_d, its Miller lines (-g1 folded in).
+// One thread per group: S = sum of the group's S_d, affine (its Miller lines,
+// -g1 folded in: k_lines_fold.hip).
 __global__ void TBG_LAUNCH k_rlc_group_lines(DevBatch B) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group;
@@ -103,8 +104,7 @@ __global__ void TBG_LAUNCH k_rlc_group_lines(DevBatch B) {
     B.grp_state[g] = GRP_FAIL;
     return;
   }
-  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.grp_lines + (size_t)LINES_WORDS * g);
+  B.pend_pts[g] = Sa;  // lines: k_lines_fold<FOLD_GROUPS>
   B.grp_state[g] = GRP_LINES;
 }
 
@@ -259,7 +259,6 @@ __global__ void TBG_LAUNCH k_rlc_resolve_groups(DevBatch B) {
 // Level 1.5 lines: one thread per listed chunk: S_c = sum of its combinable
 // duties' S_d, Miller lines with -g1 folded in.  A degenerate S_c (point at
 // infinity) flags the list entry: its candidates go straight to level 3.
-constexpr uint32_t CHUNK_DEGENERATE = 0x80000000u;
 __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= B.counters[CNT_CHUNKS]) return;
@@ -274,8 +273,7 @@ __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
     B.chunk_list[k] = qc | CHUNK_DEGENERATE;
     return;
   }
-  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.chunk_lines + (size_t)LINES_WORDS * k);
+  B.pend_pts[k] = Sa;  // lines: k_lines_fold<FOLD_CHUNKS>
 }
 
 __device__ __forceinline__ uint32_t rlc_candidates(const DevBatch& B, uint32_t d) {
@@ -379,7 +377,6 @@ __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
 
 // Level 1.5b lines, one thread per entry: S'_c = sum_d w_d S_d (suffix sums)
 // and the points w_d P_d, stored as (-x, y) for the line evaluations.
-constexpr uint32_t ID_DEGENERATE = 0x80000000u;
 __global__ void TBG_LAUNCH k_rlc_cident_lines(DevBatch B) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= B.counters[CNT_CID]) return;
@@ -406,8 +403,7 @@ __global__ void TBG_LAUNCH k_rlc_cident_lines(DevBatch B) {
     wp.x = fp_reduce(fp_neg(wp.x));
     B.cid_p[(size_t)C * j + (w - 1)] = wp;
   }
-  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.cid_lines + (size_t)LINES_WORDS * j);
+  B.pend_pts[j] = Sa;  // lines: k_lines_fold<FOLD_CID>
 }
 
 // Level 1.5b check: one quad per entry computes A'_c over the chunk's duties
@@ -489,8 +485,7 @@ __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
     return;
   }
   B.id_p[k] = Pa;
-  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines_t<true>(Sa, nx, fp_from_const(G1_NEG_Y), B.id_lines + (size_t)LINES_WORDS * k);
+  B.pend_pts[k] = Sa;  // lines: k_lines_fold<FOLD_IDENT>
 }
 
 // Level 2b check: one quad per entry computes A'_d and tests A_d^w == A'_d.
@@ -605,6 +600,7 @@ void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff
   TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B);
   uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
   TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
+  launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
 }
 
 void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
@@ -617,10 +613,13 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
       TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
+      launch_lines_fold(B, FOLD_CHUNKS, n_groups * nch, st);
       TBG_KLAUNCH(k_rlc_check_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_cident_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
+      launch_lines_fold(B, FOLD_CID, n_groups * nch, st);
       TBG_KLAUNCH(k_rlc_cident_check, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_ident_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
+      launch_lines_fold(B, FOLD_IDENT, B.n_duties, st);
       TBG_KLAUNCH(k_rlc_ident_check, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
     }
   }

@@ -435,6 +435,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_cnt = sec(4ull * CNT_WORDS);
   size_t w_pl = sec(verify ? 4ull * np : 0);
   size_t w_dvfe = sec(G > 1 ? 4ull * 3 * 4 * NL * nd : 0);
+  size_t w_pend = sec(G ? sizeof(G2A) * (size_t)std::max<size_t>(std::max<size_t>(ng, (size_t)ng * nch), nd) : 0);
   size_t w_cfe = sec(G > 1 ? 4ull * 3 * 4 * NL * ng * nch : 0);
   size_t w_cidl = sec(G > 1 ? 4ull * ng * nch : 0);
   size_t w_cidp = sec(G > 1 ? sizeof(G1A) * (size_t)ng * nch * C : 0);
@@ -558,6 +559,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.counters = (uint32_t*)(dw + w_cnt);
   B.part_list = (uint32_t*)(dw + w_pl);
   B.id_fe = (uint32_t*)(dw + w_dvfe);
+  B.pend_pts = (G2A*)(dw + w_pend);
   B.chunk_fe = (uint32_t*)(dw + w_cfe);
   B.cid_list = (uint32_t*)(dw + w_cidl);
   B.cid_p = (G1A*)(dw + w_cidp);

@@ -70,6 +70,8 @@ struct DevBatch {
   uint32_t* grp_lines;    // [n_groups][LINES_WORDS] lines of the group's S (-g1 folded in)
   uint32_t* counters;     // [CNT_*] work-list lengths
   uint32_t* part_list;    // [n_partials] level-3 partials (sig_lines by list position)
+  G2A* pend_pts;          // [max(n_groups, n_groups * chunks, n_duties)] affine points whose folded Miller
+                          // lines k_lines_fold computes next (group S, then the fallback lists' sums)
   uint32_t* chunk_fe;     // [n_groups * chunks][3][4 NL] final-exponentiated value of failed chunks (by list position)
   uint32_t* cid_list;     // [n_groups * chunks] level-1.5b entries: chunk-list positions
   G1A* cid_p;             // [n_groups * chunks][rlc_chunk] w_d P_d as (-x, y), by level-1.5b position
@@ -93,6 +95,13 @@ enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL =
 // CNT_DUTIES: level-2b duties (id_list), CNT_PARTIALS: level-3 partials, CNT_AGG: [1/D] duties,
 // CNT_CHUNKS: level-1.5 chunks, CNT_CID: level-1.5b chunks
 enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_CID = 4, CNT_WORDS = 5 };
+
+// Flags in the fallback lists (k_rlc.hip): the entry's sum is the point at
+// infinity -- no lines, its members go to an exact level.
+constexpr uint32_t CHUNK_DEGENERATE = 0x80000000u;
+constexpr uint32_t ID_DEGENERATE = 0x80000000u;
+// k_lines_fold<KIND>: which pending points get lines, and where they go.
+enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3 };
 
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {
@@ -133,6 +142,7 @@ void launch_h_lines(const DevBatch& B, hipStream_t st);
 void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
                         hipStream_t st);
 void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
+void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStream_t st);
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);
 void launch_lagrange(const DevBatch& B, hipStream_t st);
