@@ -341,15 +341,18 @@ def main():
         tickets.append(ts[0])
 
     def plan(n):
-        """Launches for exactly n steps: full launches of M batches round-robin
-        over the slots, then one launch of the first n mod M batches of the next
-        slot (a prefix of a packed device batch is a batch of its own)."""
-        full, rem = divmod(n, M)
-        ts = [tickets[k % len(tickets)] for k in range(full)]
-        ps = [0] * full
-        if rem:
-            ts.append(tickets[full % len(tickets)])
-            ps.append(rem)
+        """Launches for exactly n steps: the n batches split as evenly as the
+        slots allow over L = max(ceil(n / M), min(inflight, n)) launches
+        round-robin over the slots (a prefix of a packed device batch is a
+        batch of its own), so a short run still has `inflight` launches
+        overlapping instead of a full launch plus a small remainder."""
+        L = max(-(-n // M), min(len(tickets), n))
+        base, extra = divmod(n, L)
+        ts, ps = [], []
+        for k in range(L):
+            size = base + (1 if k < extra else 0)
+            ts.append(tickets[k % len(tickets)])
+            ps.append(0 if size == M else size)
         return ts, ps
 
     if args.warmup:
@@ -367,6 +370,7 @@ def main():
             assert batch_exact(again, b, eng)
     b = batches[0][0]
     flat = [x for g in batches for x in g]
+    group_used = e.stats(tickets[0])["group_size"]  # before api_pipeline reuses the slots (tickets expire)
 
     units = args.dvs * args.steps * ws
     value = units / elapsed
@@ -393,7 +397,7 @@ def main():
                                 f"config4: {args.t}-of-{args.n}, {args.dvs}-DV shard per GPU of the 1M-DV batch"),
                    "partials_per_step_per_gpu": args.dvs * args.n, "parallelism": f"shard{ws}",
                    "inflight_launches": args.inflight, "batches_per_launch": M,
-                   "rlc_group": e.stats(tickets[0])["group_size"],
+                   "rlc_group": group_used,
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),

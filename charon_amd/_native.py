@@ -164,6 +164,7 @@ class TbgConfig(ctypes.Structure):
         ("rlc_seed", ctypes.c_uint64),
         ("rlc_chunk", ctypes.c_uint32),
         ("streams_per_slot", ctypes.c_uint32),
+        ("rlc_batch", ctypes.c_uint32),
     ]
 
 
@@ -186,6 +187,7 @@ SIGNATURES = {
                                         ctypes.c_void_p]),
     "tbg_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_fetch_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "tbg_fetch_level0": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "tbg_last_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_sk_to_pk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     "tbg_sign": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,

@@ -27,9 +27,14 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
   } else if (KIND == FOLD_CID) {
     if (k >= B.counters[CNT_CID] || (B.cid_list[k] & ID_DEGENERATE)) return;
     out = B.cid_lines;
-  } else {
+  } else if (KIND == FOLD_IDENT) {
     if (k >= B.counters[CNT_DUTIES] || (B.id_list[k] & ID_DEGENERATE)) return;
     out = B.id_lines;
+  } else {  // FOLD_L0: level 0's S (k_msm_sum)
+    if (k != 0 || B.counters[CNT_L0_BAD]) return;
+    const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+    px_g2_lines(px_load(*B.batch_pt), nx, fp_from_const(G1_NEG_Y), B.batch_lines);
+    return;
   }
   const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
   px_g2_lines(px_load(B.pend_pts[k]), nx, fp_from_const(G1_NEG_Y), out + (size_t)LINES_WORDS * k);
@@ -42,6 +47,7 @@ void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStr
     case FOLD_GROUPS: TBG_KLAUNCH(k_lines_fold<FOLD_GROUPS>, grid, dim3(kBlock), st, B); break;
     case FOLD_CHUNKS: TBG_KLAUNCH(k_lines_fold<FOLD_CHUNKS>, grid, dim3(kBlock), st, B); break;
     case FOLD_CID: TBG_KLAUNCH(k_lines_fold<FOLD_CID>, grid, dim3(kBlock), st, B); break;
+    case FOLD_L0: TBG_KLAUNCH(k_lines_fold<FOLD_L0>, grid, dim3(kBlock), st, B); break;
     default: TBG_KLAUNCH(k_lines_fold<FOLD_IDENT>, grid, dim3(kBlock), st, B); break;
   }
 }

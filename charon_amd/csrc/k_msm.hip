@@ -1,0 +1,192 @@
+// Level 0 of the RLC schedule: the whole device batch (every caller batch
+// packed into one launch) as ONE product check
+//   prod_d e(P_d, H(m_d)) * e(-g1, S) == 1,  P_d = sum_i r_i pk_i,  S = sum_i r_i s_i,
+// before any group check (reference: the per-partial CoreVerify calls of
+// tbls.Verify / VerifyAndAggregate, tbls/tss.go:153-197, all of which a pass
+// accepts; any failure falls through to the group levels of k_rlc.hip, so
+// every verdict stays the exact per-item one).
+//
+// The signature side is the bucket MSM of bls_msm.h: 4 mixed additions per
+// partial instead of a 64-bit G2 scalar multiplication (15 doublings, 31
+// additions and a field inversion per partial at the group levels); the key
+// side uses per-key pair tables A+- = pk +- [x]pk computed once when the key
+// table is loaded, so P_d needs no inversion per partial either.
+//
+//   k_rlc_g1_l0      one lane per partial: r_i, [r_i] pk_i, bucket sizes
+//   k_msm_scan       bucket offsets (one workgroup)
+//   k_msm_scatter    bucket entries
+//   k_msm_bucket     one lane PAIR per bucket: its sum times (2j + 1)
+//   k_msm_sum        tree sums (fan-in 16), the last one in affine form
+#define TBG_ADD_DBL_INLINE 1
+#ifndef TBG_SCHED_FENCE
+#define TBG_SCHED_FENCE 1  // products in program order: fits the pair kernels in 256 VGPRs (bls_field.h)
+#endif
+#include "tbls_launch.h"
+#include "bls_msm.h"
+#include "bls_pair.h"
+
+namespace tbg {
+
+// Pair table of every usable key (k_rlc_g1_l0): A+ = pk + [x]pk, A- = pk - [x]pk.
+__global__ void TBG_LAUNCH k_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1A ap{fp_zero(), fp_zero()}, am = ap;
+  if (status[i] == DEC_OK) {
+    const G1A p0 = pk[i], x0 = xpk[i];
+    rlc_pair_from_inv(p0, x0, fp_inv(fp_reduce(fp_sub(x0.x, p0.x))), ap, am);
+  }
+  tab[2ull * i] = ap;
+  tab[2ull * i + 1] = am;
+}
+
+// Level-0 G1 side, one lane per partial: unusable keys are marked, every
+// candidate's r_i is drawn (no group lead: at level 0 two r = 1 partials of
+// different groups could cancel) and [r_i] pk_i computed from the key's pair
+// table; the four digits count into their buckets.
+__global__ void TBG_LAUNCH k_rlc_g1_l0(DevBatch B, const G1A* tab, const int32_t* pk_status, uint32_t n_pk) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B.n_partials || B.partial_status[i] != TBG_PS_NOT_VERIFIED) return;
+  const uint32_t pid = B.pubkey_ids[i];
+  if (pid >= n_pk || pk_status[pid] != DEC_OK) {
+    B.partial_status[i] = TBG_PS_ERR_PUBKEY;
+    return;
+  }
+  const uint64_t r = rlc_scalar(B.rlc_seed, i);
+  uint32_t u[4];
+  rlc_digits(r, u);
+  B.msm_r[i] = r;
+  B.part_p[i] = rlc_mul_table(tab[2ull * pid], tab[2ull * pid + 1], fp_from_const(G1_BETA), u);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    bool neg;
+    atomicAdd(&B.msm_off[msm_bucket(u[k], neg)], 1u);
+  }
+}
+
+// Exclusive scan of the bucket sizes into offsets (msm_off) and cursors
+// (msm_cur): one workgroup of 1024 lanes, 32 buckets per lane.
+constexpr int kScanBlock = 1024;
+__global__ void __launch_bounds__(kScanBlock) k_msm_scan(DevBatch B) {
+  __shared__ uint32_t part[kScanBlock];
+  constexpr uint32_t per = MSM_BUCKETS / kScanBlock;
+  const uint32_t t = threadIdx.x, j0 = t * per;
+  uint32_t sum = 0;
+  for (uint32_t j = 0; j < per; ++j) sum += B.msm_off[j0 + j];
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < kScanBlock; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t j = 0; j < per; ++j) {
+    const uint32_t c = B.msm_off[j0 + j];
+    B.msm_off[j0 + j] = run;
+    B.msm_cur[j0 + j] = run;
+    run += c;
+  }
+  if (t == kScanBlock - 1) B.msm_off[MSM_BUCKETS] = run;
+}
+
+__global__ void TBG_LAUNCH k_msm_scatter(DevBatch B) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B.n_partials || B.partial_status[i] != TBG_PS_NOT_VERIFIED) return;
+  uint32_t u[4];
+  rlc_digits(B.msm_r[i], u);
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    bool neg;
+    const uint32_t j = msm_bucket(u[k], neg);
+    B.msm_ent[atomicAdd(&B.msm_cur[j], 1u)] = msm_entry(i, k, neg);
+  }
+}
+
+// psi^k(s) (bls_msm.h) with the Fp2 coordinates split over the lane pair.
+__device__ __forceinline__ Aff<Fp2x> px_psi_k(const G2A& s, uint32_t k, bool neg) {
+  Aff<Fp2x> p = px_load(s);
+  p.y = f_reduce(p.y);  // decoded coordinates may be up to 16p (a negated root)
+  if (k & 1) p = Aff<Fp2x>{f_mulc(f_conj(p.x), PSI_X), f_mulc(f_conj(p.y), PSI_Y)};
+  const bool ny = ((k & 2) != 0) != neg;
+  if (k & 2) p.x = f_mulfp(p.x, fp_from_const(PSI2_X));
+  if (ny) p.y = f_reduce(f_neg(p.y));
+  return p;
+}
+
+// One lane pair per bucket j: the sum of its entries, times (2j + 1).
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
+  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
+  if (j >= MSM_BUCKETS) return;
+  if (B.counters[CNT_L0_BAD]) return;
+  Jac<Fp2x> acc = jac_inf<Fp2x>();
+  const uint32_t e1 = B.msm_off[j + 1];
+#pragma unroll 1
+  for (uint32_t e = B.msm_off[j]; e < e1; ++e) {
+    const uint32_t w = B.msm_ent[e];
+    acc = jac_add_aff_in(acc, px_psi_k(B.sig_aff[w >> 3], (w >> 1) & 3u, (w & 1u) != 0));
+  }
+  const uint32_t m = 2 * j + 1;
+  if (m > 1 && !jac_is_inf(acc)) {
+    const Jac<Fp2x> b = acc;
+    const int top = 31 - __builtin_clz(m);
+#pragma unroll 1
+    for (int bit = top - 1; bit >= 0; --bit) {
+      acc = jac_dbl_in(acc);
+      if ((m >> bit) & 1u) acc = jac_add_in<Fp2x, true>(acc, b);
+    }
+  }
+  px_store(B.msm_bkt[j], acc);
+}
+
+// Tree sum: lane pair t adds points [16 t, 16 t + 16) of `in` (n of them).
+// The last pass (n <= 16) writes S in affine form, or flags level 0 when S
+// is the point at infinity.
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_sum(DevBatch B, const G2J* in, uint32_t n, G2J* out) {
+  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  const uint32_t a0 = t * MSM_SUM_FAN;
+  if (a0 >= n) return;
+  if (B.counters[CNT_L0_BAD]) return;
+  const uint32_t a1 = min(a0 + MSM_SUM_FAN, n);
+  Jac<Fp2x> acc = px_load(in[a0]);
+#pragma unroll 1
+  for (uint32_t a = a0 + 1; a < a1; ++a) acc = jac_add_in<Fp2x, true>(acc, px_load(in[a]));
+  if (n > MSM_SUM_FAN) {
+    px_store(out[t], acc);
+    return;
+  }
+  if (jac_is_inf(acc)) {
+    if (pair_par() == 0) B.counters[CNT_L0_BAD] = 1;  // S = 0: no lines; the group levels decide
+    return;
+  }
+  const Fp2x zi = f_inv(acc.Z);
+  const Fp2x zi2 = f_sqr(zi);
+  px_store(*B.batch_pt, Aff<Fp2x>{f_mul(acc.X, zi2), f_mul(acc.Y, f_mul(zi2, zi))});
+}
+
+void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab, hipStream_t st) {
+  if (n) TBG_KLAUNCH(k_pubkey_tables, grid_for(n), dim3(kBlock), st, pk, xpk, status, n, tab);
+}
+
+// Level 0 up to S's lines: G1 products and P_d (k_rlc_duty_sum), then the MSM.
+void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
+  hipMemsetAsync(B.msm_off, 0, 4ull * (MSM_BUCKETS + 1), st);
+  if (B.n_partials) TBG_KLAUNCH(k_rlc_g1_l0, grid_for(B.n_partials), dim3(kBlock), st, B, pk_tab, pk_status, n_pk);
+  TBG_KLAUNCH(k_msm_scan, dim3(1), dim3(kScanBlock), st, B);
+  if (B.n_partials) TBG_KLAUNCH(k_msm_scatter, grid_for(B.n_partials), dim3(kBlock), st, B);
+  TBG_KLAUNCH(k_msm_bucket, grid_for(2 * MSM_BUCKETS), dim3(kBlock), st, B);
+  const G2J* in = B.msm_bkt;
+  uint32_t n = MSM_BUCKETS;
+  G2J* out = B.msm_sum;
+  while (true) {
+    const uint32_t m = (n + MSM_SUM_FAN - 1) / MSM_SUM_FAN;
+    TBG_KLAUNCH(k_msm_sum, grid_for(2 * m), dim3(kBlock), st, B, in, n, out);
+    if (n <= MSM_SUM_FAN) break;
+    in = out;
+    out += m;
+    n = m;
+  }
+}
+
+}  // namespace tbg

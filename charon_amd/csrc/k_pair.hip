@@ -36,6 +36,7 @@ __device__ __forceinline__ bool rlc_usable_pk(const DevBatch& B, uint32_t i, con
 // duties in one group cancel; k_rlc.hip).  Both kernels decide it the same way
 // whichever of them has already marked bad-key partials ERR_PUBKEY.
 __device__ __forceinline__ bool rlc_group_lead(const DevBatch& B, uint32_t i, const int32_t* pk_status, uint32_t n_pk) {
+  if (B.rlc_batch) return false;  // level 0 drew every r_i at random (k_msm.hip); the groups reuse them
   const uint32_t d = B.partial_duty[i];
   const uint32_t d0 = (d / B.rlc_group) * B.rlc_group;
   for (uint32_t j = B.duty_first[d0]; j < i; ++j)
@@ -57,7 +58,9 @@ __device__ __forceinline__ uint32_t u32_from_owner(uint32_t own, uint32_t j) {
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_rlc_partial2(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
                                                              const int32_t* pk_status, uint32_t n_pk) {
-  // No early return: both lanes of every pair must reach the DPP exchanges.
+  // No early return: both lanes of every pair must reach the DPP exchanges
+  // (the level-0 pass below is grid-uniform).
+  if (B.counters[CNT_L0_OK]) return;  // level 0 accepted the batch: no group levels
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool active = i < B.n_partials && B.partial_status[i] == TBG_PS_NOT_VERIFIED;
   uint32_t pid = 0;

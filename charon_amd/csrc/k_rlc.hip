@@ -54,16 +54,28 @@ __device__ __forceinline__ bool rlc_candidate(const DevBatch& B, uint32_t i) {
 // [r_i] s_i and [r_i] pk_i: k_rlc_g2_pair / k_rlc_g1 (k_pair.hip).
 
 // One thread per duty: P_d = sum r_i pk_i (affine) and S_d = sum r_i s_i.
-__global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B) {
+// Level 0 (DSUM_L0_P) forms P_d only -- its S is the batch-wide MSM -- and a
+// duty it cannot combine (P_d = 0) makes level 0 fail; after a level-0
+// failure DSUM_FALLBACK_S adds the S_d of the duties level 0 combined (the
+// stored P-chunk products include them; S_d = 0 is just a term of the sums).
+__global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B, int phase) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= B.n_duties) return;
+  if (phase == DSUM_FALLBACK_S) {
+    if (B.counters[CNT_L0_OK] || B.dv_state[d] != RLC_COMBINED) return;
+    G2J S = jac_inf<Fp2>();
+    for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i)
+      if (rlc_candidate(B, i)) S = jac_add(S, B.part_s[i]);
+    B.dv_s[d] = S;
+    return;
+  }
   G1J P = jac_inf<Fp>();
   G2J S = jac_inf<Fp2>();
   int cand = 0;
   for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) {
     if (!rlc_candidate(B, i)) continue;
     P = jac_add(P, B.part_p[i]);
-    S = jac_add(S, B.part_s[i]);
+    if (phase == DSUM_BOTH) S = jac_add(S, B.part_s[i]);
     ++cand;
   }
   if (cand == 0) {
@@ -71,18 +83,20 @@ __global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B) {
     return;
   }
   G1A Pa;
-  if (!jac_to_aff(P, Pa) || jac_is_inf(S)) {
+  if (!jac_to_aff(P, Pa) || (phase == DSUM_BOTH && jac_is_inf(S))) {
     B.dv_state[d] = RLC_EACH;  // degenerate combination: check the partials one by one
+    if (phase == DSUM_L0_P) B.counters[CNT_L0_BAD] = 1;
     return;
   }
   B.dv_p[d] = Pa;
-  B.dv_s[d] = S;
+  if (phase == DSUM_BOTH) B.dv_s[d] = S;
   B.dv_state[d] = RLC_COMBINED;
 }
 
 // One thread per group: S = sum of the group's S_d, affine (its Miller lines,
 // -g1 folded in: k_lines_fold.hip).
 __global__ void TBG_LAUNCH k_rlc_group_lines(DevBatch B) {
+  if (B.counters[CNT_L0_OK]) return;  // level 0 accepted the batch (k_l0_after set the groups)
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
@@ -155,33 +169,62 @@ __device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
 // spread over several quads -- and because the P pairs of a chunk are kept
 // apart from S, a failed group can re-check its chunks (level 1.5) from these
 // same products with only S_c's Miller loop added.
-__global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
+//   MILLER_GROUPS   P chunks, then every group's S quad (no level 0);
+//   MILLER_L0       P chunks, then ONE quad for level 0's S (batch_f);
+//   MILLER_GROUP_S  after a level-0 failure: the groups' S quads only (the P
+//                   chunk products of level 0 serve the group checks as they are).
+__global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B, int mode) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
   uint32_t nch = (G + C - 1) / C, nq = nch + 1;
-  // P chunks first, then every group's S quad: S quads evaluate one line per
-  // step instead of C, and in waves of their own they finish early instead of
+  // P chunks first, then the S quads: S quads evaluate one line per step
+  // instead of C, and in waves of their own they finish early instead of
   // each holding a P chunk's wave slot for its full length
   uint32_t qd = t >> 2;
-  if (qd >= n_groups * nq) return;
   const uint32_t np_q = n_groups * nch;
-  uint32_t g = qd < np_q ? qd / nch : qd - np_q, c = qd < np_q ? qd % nch : nch;
-  qd = g * nq + c;  // storage index
-  // a group whose S sum degenerated (GRP_FAIL here) still gets its P-chunk
-  // products: level 1.5 re-checks its chunks from them
-  const int32_t gs = B.grp_state[g];
-  if (gs == GRP_EMPTY || (gs == GRP_FAIL && c == nch)) return;
-  uint32_t gd1 = min(g * G + G, B.n_duties);
-  uint32_t d0 = g * G + c * C, d1 = c == nch ? d0 : min(d0 + C, gd1);
-  const uint32_t* ls = B.grp_lines + (size_t)LINES_WORDS * g;
+  uint32_t g, c;
+  bool l0_s = false;
+  if (mode == MILLER_GROUP_S) {
+    if (B.counters[CNT_L0_OK] || qd >= n_groups) return;
+    g = qd;
+    c = nch;
+  } else {
+    if (qd >= (mode == MILLER_L0 ? np_q + 1 : n_groups * nq)) return;
+    l0_s = mode == MILLER_L0 && qd == np_q;
+    g = qd < np_q ? qd / nch : qd - np_q;
+    c = qd < np_q ? qd % nch : nch;
+  }
+  const uint32_t* ls;
+  uint32_t* dst;
+  uint32_t d0 = 0, d1 = 0;
+  if (l0_s) {
+    if (B.counters[CNT_L0_BAD]) return;
+    ls = B.batch_lines;
+    dst = B.batch_f;
+  } else {
+    qd = g * nq + c;  // storage index
+    // a group whose S sum degenerated (GRP_FAIL here) still gets its P-chunk
+    // products: level 1.5 re-checks its chunks from them.  (Level 0's P
+    // chunks run before any group state exists.)
+    if (mode != MILLER_L0) {
+      const int32_t gs = B.grp_state[g];
+      if (gs == GRP_EMPTY || (gs == GRP_FAIL && c == nch)) return;
+    }
+    uint32_t gd1 = min(g * G + G, B.n_duties);
+    d0 = g * G + c * C;
+    d1 = c == nch ? d0 : min(d0 + C, gd1);
+    ls = B.grp_lines + (size_t)LINES_WORDS * g;
+    dst = B.chunk_f + (size_t)3 * QUAD_WORDS * qd;
+  }
+  const bool s_quad = l0_s || c == nch;
   Fp4 f = quad_one();
   int idx = 0;
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = quad_sqr_in(f);
     int steps = ((X_ABS >> b) & 1) ? 2 : 1;
     for (int s = 0; s < steps; ++s, ++idx) {
-      if (c == nch) f = quad_line_folded<true>(f, ls, idx);
+      if (s_quad) f = quad_line_folded<true>(f, ls, idx);
       for (uint32_t d = d0; d < d1; ++d) {
         if (B.dv_state[d] != RLC_COMBINED) continue;
         uint32_t m = B.duty_msg[d];
@@ -191,7 +234,7 @@ __global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
       }
     }
   }
-  quad_store(B.chunk_f + (size_t)3 * QUAD_WORDS * qd, f);
+  quad_store(dst, f);
 }
 
 // Level 1, final part: one quad per group multiplies its chunks' products
@@ -218,6 +261,62 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
   f = quad_final_exp_in(quad_conj(f));
   bool ok = quad_is_one(f);
   if (lead) B.grp_state[g] = ok ? GRP_OK : GRP_FAIL;
+}
+
+// ------------------------------------------------------------------ level 0
+// One quad per group: the product of its P-chunk values (k_rlc_miller_chunks,
+// MILLER_L0); a combined duty whose H(m) is unusable makes level 0 fail.
+__global__ void TBG_LAUNCH k_l0_fold(DevBatch B) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk;
+  const uint32_t n_groups = (B.n_duties + G - 1) / G, nch = (G + C - 1) / C, nq = nch + 1;
+  const uint32_t g = t >> 2;
+  if (g >= n_groups || B.counters[CNT_L0_BAD]) return;
+  const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
+  for (uint32_t d = d0; d < d1; ++d) {
+    if (B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] != 0) {
+      if ((t & 3) == 0) B.counters[CNT_L0_BAD] = 1;
+      return;
+    }
+  }
+  const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nq * g;
+  Fp4 f = quad_load(base);
+  for (uint32_t c = 1; c < nch; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
+  quad_store(B.grp_f + (size_t)3 * QUAD_WORDS * g, f);
+}
+
+// Product tree, one quad per L0_TREE_FAN values of grp_f[in .. in + n).
+__global__ void TBG_LAUNCH k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32_t out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = t >> 2, a0 = q * L0_TREE_FAN;
+  if (a0 >= n || B.counters[CNT_L0_BAD]) return;
+  const uint32_t a1 = min(a0 + L0_TREE_FAN, n);
+  Fp4 f = quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a0));
+  for (uint32_t a = a0 + 1; a < a1; ++a) f = quad_mul(f, quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
+  quad_store(B.grp_f + (size_t)3 * QUAD_WORDS * (out + q), f);
+}
+
+// One quad: the last <= L0_TREE_FAN values times the S pair's product, one
+// final exponentiation for the whole batch.
+__global__ void TBG_LAUNCH k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
+  if (threadIdx.x >= 4 || B.counters[CNT_L0_BAD]) return;
+  Fp4 f = quad_load(B.batch_f);
+  for (uint32_t a = 0; a < n; ++a) f = quad_mul(f, quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
+  f = quad_final_exp_in(quad_conj(f));
+  const bool ok = quad_is_one(f);
+  if (ok && threadIdx.x == 0) B.counters[CNT_L0_OK] = 1;
+}
+
+// One thread per group: after a level-0 pass every group with a combined
+// duty is accepted (k_rlc_resolve_groups marks its candidates valid).
+__global__ void TBG_LAUNCH k_l0_after(DevBatch B) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t G = B.rlc_group;
+  if (g >= (B.n_duties + G - 1) / G || !B.counters[CNT_L0_OK]) return;
+  const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
+  bool any = false;
+  for (uint32_t d = d0; d < d1; ++d) any |= B.dv_state[d] == RLC_COMBINED;
+  B.grp_state[g] = any ? GRP_OK : GRP_EMPTY;
 }
 
 __device__ __forceinline__ void rlc_mark(const DevBatch& B, uint32_t d, int32_t st) {
@@ -589,26 +688,56 @@ __global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   if (lead) B.partial_status[i] = ok ? TBG_PS_VALID : TBG_PS_INVALID;
 }
 
-void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
-                        hipStream_t st) {
+void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const G1A* pk_tab,
+                        const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
   if (!B.n_duties) return;
   if (B.rlc_group == 0) {
     if (B.n_partials) TBG_KLAUNCH(k_list_all_partials, grid_for(B.n_partials), dim3(kBlock), st, B, pk_status, n_pk);
     return;
   }
-  launch_rlc_partials(B, pk_aff, xpk_aff, pk_status, n_pk, st);
-  TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B);
   uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
+  if (B.rlc_batch) {  // level 0: G1 products, P_d, the signature MSM and S's lines
+    launch_l0_prepare(B, pk_tab, pk_status, n_pk, st);
+    TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B, (int)DSUM_L0_P);
+    launch_lines_fold(B, FOLD_L0, 1, st);
+    return;
+  }
+  launch_rlc_partials(B, pk_aff, xpk_aff, pk_status, n_pk, st);
+  TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B, (int)DSUM_BOTH);
   TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
   launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
 }
 
-void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
+void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
+                      hipStream_t st) {
   if (!B.n_duties) return;
   if (B.rlc_group != 0) {
     uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
-    TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups * (nch + 1)), dim3(kBlock), st, B);
+    if (B.rlc_batch) {
+      // level 0: the P chunks (kept for the group levels) and S, one product
+      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * (n_groups * nch + 1)), dim3(kBlock), st, B, (int)MILLER_L0);
+      TBG_KLAUNCH(k_l0_fold, grid_for(4 * n_groups), dim3(kBlock), st, B);
+      uint32_t in = 0, n = n_groups, out = n_groups;
+      while (n > L0_TREE_FAN) {
+        const uint32_t m = (n + L0_TREE_FAN - 1) / L0_TREE_FAN;
+        TBG_KLAUNCH(k_l0_tree, grid_for(4 * m), dim3(kBlock), st, B, in, n, out);
+        in = out;
+        out += m;
+        n = m;
+      }
+      TBG_KLAUNCH(k_l0_final, dim3(1), dim3(kBlock), st, B, in, n);
+      TBG_KLAUNCH(k_l0_after, grid_for(n_groups), dim3(kBlock), st, B);
+      // level 0 failed: the group levels' signature side (these kernels
+      // return at once after a pass)
+      launch_rlc_partials(B, pk_aff, xpk_aff, pk_status, n_pk, st);
+      TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B, (int)DSUM_FALLBACK_S);
+      TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
+      launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
+      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups), dim3(kBlock), st, B, (int)MILLER_GROUP_S);
+    } else {
+      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups * (nch + 1)), dim3(kBlock), st, B, (int)MILLER_GROUPS);
+    }
     TBG_KLAUNCH(k_rlc_group_final, grid_for(4 * n_groups), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {

@@ -80,6 +80,7 @@ struct tbg_ctx {
   std::mutex mu;
   G1A* d_pk = nullptr;
   G1A* d_xpk = nullptr;  // [x] pk per entry (k_decode_pubkeys)
+  G1A* d_pktab = nullptr;  // [2 per entry] pk + [x]pk, pk - [x]pk (level 0's G1 products, k_msm.hip)
   int32_t* d_pk_status = nullptr;
   uint32_t n_pk = 0, cap_pk = 0;
   std::vector<void*> retired;  // outgrown pubkey tables (see tbg_load_pubkeys)
@@ -92,6 +93,7 @@ struct tbg_ctx {
   uint32_t rlc_group = 16;  // 0 = per-partial checks (TBG_VERIFY_EACH)
   uint32_t rlc_chunk = 4;
   bool rlc_auto = false;     // rlc_group follows the observed invalid share (tbg_config.rlc_group = 0)
+  uint32_t rlc_batch = TBG_RLC_L0_AUTO;  // level 0 (the whole device batch as one check)
   double invalid_ema = 0.0;  // exponential average of the invalid share of collected verified partials
   uint64_t rlc_seed = 0;   // 0 = OS randomness per batch
   uint64_t seed_ctr = 0;
@@ -164,6 +166,8 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   else c->rlc_auto = true;
   if (cfg && cfg->rlc_chunk) c->rlc_chunk = cfg->rlc_chunk;
   if (c->rlc_group > 4096 || c->rlc_chunk > 4096) { delete c; return TBG_E_INVALID_ARG; }
+  if (cfg && cfg->rlc_batch > TBG_RLC_L0_OFF) { delete c; return TBG_E_INVALID_ARG; }
+  if (cfg) c->rlc_batch = cfg->rlc_batch;
   c->rlc_seed = cfg ? cfg->rlc_seed : 0;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -218,6 +222,7 @@ void tbg_destroy(tbg_ctx* c) {
   }
   if (c->d_pk) hipFree(c->d_pk);
   if (c->d_xpk) hipFree(c->d_xpk);
+  if (c->d_pktab) hipFree(c->d_pktab);
   if (c->d_pk_status) hipFree(c->d_pk_status);
   for (void* p : c->retired) hipFree(p);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -236,13 +241,21 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
     uint32_t ncap = need + need / 2 + 1024;
     G1A* npk = nullptr;
     G1A* nxpk = nullptr;
+    G1A* ntab = nullptr;
     int32_t* nst = nullptr;
     if (hipMalloc(&npk, sizeof(G1A) * (size_t)ncap) != hipSuccess) return TBG_E_OOM;
     if (hipMalloc(&nxpk, sizeof(G1A) * (size_t)ncap) != hipSuccess) { hipFree(npk); return TBG_E_OOM; }
-    if (hipMalloc(&nst, sizeof(int32_t) * (size_t)ncap) != hipSuccess) { hipFree(npk); hipFree(nxpk); return TBG_E_OOM; }
+    if (hipMalloc(&ntab, 2 * sizeof(G1A) * (size_t)ncap) != hipSuccess) { hipFree(npk); hipFree(nxpk); return TBG_E_OOM; }
+    if (hipMalloc(&nst, sizeof(int32_t) * (size_t)ncap) != hipSuccess) {
+      hipFree(npk);
+      hipFree(nxpk);
+      hipFree(ntab);
+      return TBG_E_OOM;
+    }
     if (c->n_pk) {
       HIP_TRY(hipMemcpyAsync(npk, c->d_pk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
       HIP_TRY(hipMemcpyAsync(nxpk, c->d_xpk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(ntab, c->d_pktab, 2 * sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
       HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -252,9 +265,11 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
     // the final one.
     if (c->d_pk) c->retired.push_back(c->d_pk);
     if (c->d_xpk) c->retired.push_back(c->d_xpk);
+    if (c->d_pktab) c->retired.push_back(c->d_pktab);
     if (c->d_pk_status) c->retired.push_back(c->d_pk_status);
     c->d_pk = npk;
     c->d_xpk = nxpk;
+    c->d_pktab = ntab;
     c->d_pk_status = nst;
     c->cap_pk = ncap;
   }
@@ -266,6 +281,8 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   if (hipMemcpyAsync(d_bytes, pk48, 48ull * count, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
   if (rc == TBG_OK) {
     launch_decode_pubkeys(d_bytes, count, c->d_pk + c->n_pk, c->d_xpk + c->n_pk, c->d_pk_status + c->n_pk, c->stream);
+    launch_pubkey_tables(c->d_pk + c->n_pk, c->d_xpk + c->n_pk, c->d_pk_status + c->n_pk, count,
+                         c->d_pktab + 2ull * c->n_pk, c->stream);
     if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
   }
   if (rc == TBG_OK && status &&
@@ -298,11 +315,12 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   HIP_TRY(hipMemsetAsync(B.counters, 0, 4 * CNT_WORDS, st));
   launch_decode_sigs(B, st);
   HIP_TRY(hipEventRecord(ev[1], st));
-  if (verify) launch_rlc_prepare(B, pk, (const G1A*)c->d_xpk, (const int32_t*)c->d_pk_status, c->n_pk, st);
+  if (verify)
+    launch_rlc_prepare(B, pk, (const G1A*)c->d_xpk, (const G1A*)c->d_pktab, (const int32_t*)c->d_pk_status, c->n_pk, st);
   HIP_TRY(hipEventRecord(ev[2], st));
   HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
   HIP_TRY(hipEventRecord(ev[6], st));
-  if (verify) launch_rlc_check(B, pk, st);
+  if (verify) launch_rlc_check(B, pk, (const G1A*)c->d_xpk, (const int32_t*)c->d_pk_status, c->n_pk, st);
   HIP_TRY(hipEventRecord(ev[7], st));
   if (B.op != TBG_OP_VERIFY) launch_lagrange(B, st);
   HIP_TRY(hipEventRecord(ev[8], st));
@@ -422,6 +440,10 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   const uint32_t ng = G ? (nd + G - 1) / G : 0;
   const uint32_t C = c->rlc_chunk < G ? c->rlc_chunk : (G ? G : 1);
   const uint32_t nch = G ? (G + C - 1) / C : 0;
+  // Level 0 while the collected batches are clean (or as configured): one
+  // failed level-0 check costs its own work on top of the group levels.
+  const bool l0 = G != 0 && np < (1u << 28) &&
+                  (c->rlc_batch == TBG_RLC_L0_ON || (c->rlc_batch == TBG_RLC_L0_AUTO && c->invalid_ema < TBG_RLC_AUTO_L0));
   size_t w_pp = sec(G ? sizeof(G1J) * (size_t)np : 0);
   size_t w_ps = sec(G ? sizeof(G2J) * (size_t)np : 0);
   size_t w_cf = sec(G ? 4ull * 3 * 4 * NL * ng * (nch + 1) : 0);
@@ -442,6 +464,16 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_cidlines = sec(G > 1 ? 4ull * LINES_WORDS * ng * nch : 0);
   size_t w_idl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_idp = sec(G > 1 ? sizeof(G1A) * (size_t)nd : 0);
+  size_t w_mr = sec(l0 ? 8ull * np : 0);
+  size_t w_moff = sec(l0 ? 4ull * (MSM_BUCKETS + 1) : 0);
+  size_t w_mcur = sec(l0 ? 4ull * MSM_BUCKETS : 0);
+  size_t w_ment = sec(l0 ? 16ull * np : 0);
+  size_t w_mbkt = sec(l0 ? sizeof(G2J) * (size_t)MSM_BUCKETS : 0);
+  size_t w_msum = sec(l0 ? sizeof(G2J) * (size_t)MSM_SUM_ENTRIES : 0);
+  size_t w_bpt = sec(l0 ? sizeof(G2A) : 0);
+  size_t w_blines = sec(l0 ? 4ull * LINES_WORDS : 0);
+  size_t w_bf = sec(l0 ? 4ull * 3 * 4 * NL : 0);
+  size_t w_gf = sec(l0 ? 4ull * 3 * 4 * NL * grp_f_entries(ng) : 0);
   size_t w_aacc = sec(op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
   size_t w_alist = sec(op != TBG_OP_VERIFY ? 4ull * nd : 0);
   size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
@@ -570,6 +602,17 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.partial_status = (int32_t*)(dw + w_pst);
   B.duty_status = (int32_t*)(dw + w_dst);
   B.agg = dw + w_agg;
+  B.rlc_batch = l0 ? 1u : 0u;
+  B.msm_r = (uint64_t*)(dw + w_mr);
+  B.msm_off = (uint32_t*)(dw + w_moff);
+  B.msm_cur = (uint32_t*)(dw + w_mcur);
+  B.msm_ent = (uint32_t*)(dw + w_ment);
+  B.msm_bkt = (G2J*)(dw + w_mbkt);
+  B.msm_sum = (G2J*)(dw + w_msum);
+  B.batch_pt = (G2A*)(dw + w_bpt);
+  B.batch_lines = (uint32_t*)(dw + w_blines);
+  B.batch_f = (uint32_t*)(dw + w_bf);
+  B.grp_f = (uint32_t*)(dw + w_gf);
   B.agg_acc = (G2J*)(dw + w_aacc);
   B.agg_list = (uint32_t*)(dw + w_alist);
 
@@ -656,7 +699,7 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     return TBG_E_DEVICE;
   }
   copy_part(s, *q, pst, dst, agg);
-  if (c->rlc_auto && s->op != TBG_OP_AGGREGATE && q->np) {  // the adaptive group size's input
+  if (s->op != TBG_OP_AGGREGATE && q->np) {  // the adaptive group size's and level 0's input
     const int32_t* st = (const int32_t*)s->h_out;  // partial statuses lead the output region
     uint32_t bad = 0;
     for (uint32_t i = 0; i < q->np; ++i) bad += st[q->p0 + i] == TBG_PS_INVALID ? 1u : 0u;
@@ -766,6 +809,21 @@ int tbg_fetch_stats(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
   out4[1] = cnt[CNT_DUTIES];
   out4[2] = cnt[CNT_PARTIALS];
   out4[3] = s->B.rlc_group;
+  return TBG_OK;
+}
+
+int tbg_fetch_level0(tbg_ctx* c, tbg_ticket t, int32_t* state) {
+  if (!c || !state) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = find_ticket(c, t, false, nullptr);
+  if (!s) return TBG_E_TICKET;
+  *state = TBG_L0_NOT_RUN;
+  if (s->op == TBG_OP_AGGREGATE || !s->B.rlc_batch) return TBG_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  uint32_t cnt[CNT_WORDS] = {};
+  HIP_TRY(hipMemcpyAsync(cnt, s->B.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
+  HIP_TRY(hipStreamSynchronize(s->st));
+  *state = cnt[CNT_L0_OK] ? TBG_L0_PASSED : TBG_L0_FAILED;
   return TBG_OK;
 }
 
@@ -1051,8 +1109,8 @@ int tbg_fast_aggregate_verify(tbg_ctx* c, const uint32_t* pubkey_ids, const uint
   tbg::launch_decode_sigs(B, st);
   tbg::launch_hash_msgs(B, st);
   tbg::launch_h_lines(B, st);
-  tbg::launch_rlc_prepare(B, t_pk, t_xpk, t_pkst, n, st);
-  tbg::launch_rlc_check(B, t_pk, st);
+  tbg::launch_rlc_prepare(B, t_pk, t_xpk, nullptr, t_pkst, n, st);
+  tbg::launch_rlc_check(B, t_pk, t_xpk, t_pkst, n, st);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(status, B.partial_status, 4ull * n, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));

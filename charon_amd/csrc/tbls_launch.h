@@ -81,6 +81,21 @@ struct DevBatch {
   G1A* id_p;              // [n_duties] sum w_i r_i pk_i (affine), by level-2b position
   uint32_t* id_lines;     // lines of sum w_i r_i sig_i by level-2b position: aliases sig_lines,
                           // which level 3 only fills after level 2b has consumed them
+  // level 0 (k_msm.hip, k_rlc.hip): the whole device batch as ONE RLC check,
+  //   prod_d e(P_d, H(m_d)) * e(-g1, S) == 1,  S = sum_i r_i s_i,
+  // S as a bucket MSM over the signatures and their psi images (no per-partial
+  // G2 scalar multiplication); a failure falls through to the group levels
+  uint32_t rlc_batch;     // 1: level 0 runs first (every candidate's r_i random, no group lead)
+  uint64_t* msm_r;        // [n_partials] r_i of the candidates
+  uint32_t* msm_off;      // [MSM_BUCKETS + 1] bucket sizes, then their offsets
+  uint32_t* msm_cur;      // [MSM_BUCKETS] scatter cursors
+  uint32_t* msm_ent;      // [4 n_partials] bucket entries: partial << 3 | k << 1 | negative
+  G2J* msm_bkt;           // [MSM_BUCKETS] (2j + 1) * (bucket j's sum)
+  G2J* msm_sum;           // [MSM_SUM_ENTRIES] tree sums of msm_bkt
+  G2A* batch_pt;          // [1] S in affine form
+  uint32_t* batch_lines;  // [LINES_WORDS] Miller lines of S (-g1 folded in)
+  uint32_t* batch_f;      // [3][4 NL] Miller product of the S pair (quad layout)
+  uint32_t* grp_f;        // [GRP_F_ENTRIES(n_groups)][3][4 NL] each group's P-chunk product, then the product tree
   // recombination (k_aggregate.hip)
   G2J* agg_acc;           // [n_duties] integer-coefficient sums awaiting [1/D] (listed duties only)
   uint32_t* agg_list;     // [n_duties] duties whose Lagrange denominator D > 1
@@ -93,15 +108,30 @@ struct DevBatch {
 enum RlcState : int32_t { RLC_NONE = 0, RLC_COMBINED = 1, RLC_EACH = 2 };
 enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3 };
 // CNT_DUTIES: level-2b duties (id_list), CNT_PARTIALS: level-3 partials, CNT_AGG: [1/D] duties,
-// CNT_CHUNKS: level-1.5 chunks, CNT_CID: level-1.5b chunks
-enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_CID = 4, CNT_WORDS = 5 };
+// CNT_CHUNKS: level-1.5 chunks, CNT_CID: level-1.5b chunks, CNT_L0_BAD: level 0 cannot
+// hold (a degenerate sum, a duty checked per partial, an unusable H(m)), CNT_L0_OK: level 0 passed
+enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_CID = 4, CNT_L0_BAD = 5,
+                     CNT_L0_OK = 6, CNT_WORDS = 7 };
+
+// Level-0 MSM: a digit a (odd, |a| < 2^16) of r_i puts psi^k(s_i) into bucket
+// (|a| - 1) / 2; the tree sums fold MSM_SUM_FAN points per thread.
+constexpr uint32_t MSM_BUCKETS = 32768;
+constexpr uint32_t MSM_SUM_FAN = 16;
+constexpr uint32_t MSM_SUM_ENTRIES = MSM_BUCKETS / MSM_SUM_FAN + MSM_BUCKETS / (MSM_SUM_FAN * MSM_SUM_FAN) + 16;
+// Level-0 product tree over the groups' P-chunk products (fan-in 16 per quad).
+constexpr uint32_t L0_TREE_FAN = 16;
+TBG_HD inline uint32_t grp_f_entries(uint32_t n_groups) { return n_groups + n_groups / (L0_TREE_FAN - 1) + 2 * L0_TREE_FAN; }
+// k_rlc_miller_chunks modes
+enum MillerMode : int { MILLER_GROUPS = 0, MILLER_L0 = 1, MILLER_GROUP_S = 2 };
+// k_rlc_duty_sum phases
+enum DutySumPhase : int { DSUM_BOTH = 0, DSUM_L0_P = 1, DSUM_FALLBACK_S = 2 };
 
 // Flags in the fallback lists (k_rlc.hip): the entry's sum is the point at
 // infinity -- no lines, its members go to an exact level.
 constexpr uint32_t CHUNK_DEGENERATE = 0x80000000u;
 constexpr uint32_t ID_DEGENERATE = 0x80000000u;
 // k_lines_fold<KIND>: which pending points get lines, and where they go.
-enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3 };
+enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3, FOLD_L0 = 4 };
 
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {
@@ -139,10 +169,15 @@ void launch_decode_sigs(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);
 void launch_hash_clear(const DevBatch& B, hipStream_t st);
 void launch_h_lines(const DevBatch& B, hipStream_t st);
-void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
-                        hipStream_t st);
-void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
+void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const G1A* pk_tab,
+                        const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
+                      hipStream_t st);
 void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStream_t st);
+// level 0 (k_msm.hip)
+void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab, hipStream_t st);
+void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+void launch_l0_check(const DevBatch& B, hipStream_t st);
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);
 void launch_lagrange(const DevBatch& B, hipStream_t st);

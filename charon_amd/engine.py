@@ -25,6 +25,8 @@ OP_VERIFY, OP_AGGREGATE, OP_VERIFY_AGGREGATE = 1, 2, 3
 NO_PUBKEY = 0xFFFFFFFF
 TIMING_KEYS = ["decode", "hash", "combine", "h_lines", "verify", "lagrange", "aggregate", "total"]
 VERIFY_RLC, VERIFY_EACH = 0, 1
+RLC_L0_AUTO, RLC_L0_ON, RLC_L0_OFF = 0, 1, 2   # tbg_config.rlc_batch
+L0_NOT_RUN, L0_PASSED, L0_FAILED = 0, 1, 2     # tbg_fetch_level0
 E_PENDING = -6
 
 
@@ -69,11 +71,11 @@ class Engine:
     """One context = one GPU (HIP device ordinal)."""
 
     def __init__(self, device: int = 0, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0,
-                 rlc_seed: int = 0, rlc_chunk: int = 0, streams_per_slot: int = 0):
+                 rlc_seed: int = 0, rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
-                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot)
+                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch)
         h = ctypes.c_void_p()
         rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
         self._check(rc, "tbg_init")
@@ -211,6 +213,12 @@ class Engine:
         self._check(self._lib.tbg_fetch_stats(self._h, ticket, _ptr(out)), "tbg_fetch_stats")
         return dict(zip(["groups", "duty_checks", "partial_checks", "group_size"], out.tolist()))
 
+    def level0(self, ticket) -> int:
+        """Level 0 of the batch's last run: L0_NOT_RUN, L0_PASSED or L0_FAILED."""
+        st = ctypes.c_int32(0)
+        self._check(self._lib.tbg_fetch_level0(self._h, ticket, ctypes.byref(st)), "tbg_fetch_level0")
+        return st.value
+
     def timings(self):
         ms = np.zeros(8, dtype=np.float32)
         self._check(self._lib.tbg_last_timings(self._h, _ptr(ms)), "tbg_last_timings")
@@ -275,11 +283,11 @@ class MultiEngine:
     (several contexts on one GPU)."""
 
     def __init__(self, devices, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0, rlc_seed: int = 0,
-                 rlc_chunk: int = 0, streams_per_slot: int = 0):
+                 rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=0, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
-                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot)
+                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch)
         devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
         h = ctypes.c_void_p()
         rc = self._lib.tbg_multi_init(ctypes.byref(cfg), _ptr(devs), len(devs), ctypes.byref(h))

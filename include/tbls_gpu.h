@@ -89,6 +89,9 @@ typedef struct {
   uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests) */
   uint32_t rlc_chunk;     /* duties per Miller-loop quad inside a group (0 -> 4)  */
   uint32_t streams_per_slot; /* 1 (0 -> 1) or 2: hash_to_G2 on its own stream   */
+  uint32_t rlc_batch;     /* level 0, the whole device batch as ONE check (RLC mode):
+                           * TBG_RLC_L0_AUTO (0) while the collected batches are clean,
+                           * TBG_RLC_L0_ON always, TBG_RLC_L0_OFF never              */
 } tbg_config;
 
 /* Verification schedule.  Both give every partial the verdict of the exact
@@ -103,6 +106,20 @@ typedef struct {
  * at 0 % 16 beats 8 by 6 %). */
 #define TBG_RLC_AUTO_TO8 0.003
 #define TBG_RLC_AUTO_TO4 0.03
+/* Level 0 (rlc_batch): every candidate of the device batch (all batches of
+ * one tbg_submit_group) in one product check whose signature side is a
+ * bucket multi-scalar multiplication -- no per-partial G2 scalar
+ * multiplication; a failure falls through to the group levels.  AUTO runs it
+ * while the invalid-share average is below TBG_RLC_AUTO_L0 (a failed level
+ * 0 costs ~10 % on top of the group levels; a pass saves ~20 %). */
+#define TBG_RLC_L0_AUTO 0
+#define TBG_RLC_L0_ON 1
+#define TBG_RLC_L0_OFF 2
+#define TBG_RLC_AUTO_L0 2e-6
+/* tbg_fetch_level0 states */
+#define TBG_L0_NOT_RUN 0
+#define TBG_L0_PASSED 1
+#define TBG_L0_FAILED 2
 
 /* A batch of DV-duties in structure-of-arrays form.
  * Duty d owns partials [duty_first[d], duty_first[d+1]) and message duty_msg[d];
@@ -181,6 +198,10 @@ int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t*
  * failed duties searched for their invalid partial (level 2b), partials
  * checked one by one (level 3), duties per group (0 = TBG_VERIFY_EACH)]. */
 int tbg_fetch_stats(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out4);
+/* Level 0 of a collected batch's last run: *state = TBG_L0_NOT_RUN,
+ * TBG_L0_PASSED (every candidate accepted by the one batch-wide check) or
+ * TBG_L0_FAILED (the group levels decided). */
+int tbg_fetch_level0(tbg_ctx* ctx, tbg_ticket ticket, int32_t* state);
 
 /* Plain BLS aggregation (every coefficient 1) for the DKG / cluster-lock
  * multi-signatures: AggregatePublicKeys / AggregateSignatures of

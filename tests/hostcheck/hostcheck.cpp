@@ -543,3 +543,23 @@ extern "C" int hc_base_x_check(const uint8_t* sig96, const uint32_t* k_words, ui
   const G2J p = jac_from_aff(s);
   return jac_eq(g2_mul_base_x(p, d), jac_mul_words(p, w, 256)) ? 1 : 0;
 }
+
+#include "../../charon_amd/csrc/bls_msm.h"
+// Level-0 bucket MSM (k_msm.hip) against the per-partial RLC products:
+// sum_i [r_i] s_i by buckets == sum_i rlc_mul_g2(s_i, digits(r_i)).
+extern "C" {
+int hc_msm_check(const uint8_t* sigs96, const uint64_t* r, uint32_t n) {
+  static G2J buckets[32768];
+  G2A s[64];
+  if (n > 64) return -2;
+  G2J ref = jac_inf<Fp2>();
+  for (uint32_t i = 0; i < n; ++i) {
+    if (g2_decompress(sigs96 + 96ull * i, s[i]) != DEC_OK) return -1;
+    uint32_t a[4];
+    rlc_digits(r[i], a);
+    ref = jac_add(ref, rlc_mul_g2(s[i], a));
+  }
+  G2J got = msm_reference(s, r, n, buckets);
+  return jac_eq(got, ref) ? 1 : 0;
+}
+}  // extern "C"

@@ -34,8 +34,13 @@ SCHEDULES = {
     # the default: adaptive group size (16 while clean, 8 / 4 after invalid
     # batches), 4 duties per Miller quad, fresh OS randomness per batch
     "rlc16": dict(verify_mode=0),
-    # the previous default: 8 duties per group, 2 per quad
-    "rlc8c2": dict(verify_mode=0, rlc_group=8, rlc_chunk=2, rlc_seed=0x8C2),
+    # the previous default: 8 duties per group, 2 per quad; no level 0 (the
+    # group levels alone, with their r = 1 group leads)
+    "rlc8c2": dict(verify_mode=0, rlc_group=8, rlc_chunk=2, rlc_seed=0x8C2, rlc_batch=2),
+    # level 0 on every batch: one batch-wide check (bucket MSM of the
+    # signatures), injected batches fall through to the group levels
+    "l0g16": dict(verify_mode=0, rlc_group=16, rlc_batch=1, rlc_seed=0x10),
+    "l0g7c3": dict(verify_mode=0, rlc_group=7, rlc_chunk=3, rlc_batch=1, rlc_seed=0x703),
     # large groups: most injected failures fall back through all three levels
     "rlc64": dict(verify_mode=0, rlc_group=64, rlc_seed=0xC0FFEE),
     # odd group / chunk sizes: ragged last group, chunks of 3 duties
@@ -183,6 +188,7 @@ def test_clean_batch_needs_no_fallback(engine):
                       duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
     res = engine.collect(t)
     assert (res.partial_status == eng.PS_VALID).all()
+    assert engine.level0(t) in (eng.L0_NOT_RUN, eng.L0_PASSED)  # a clean batch never fails level 0
     st = engine.stats(t)
     if st["group_size"]:
         assert st["duty_checks"] == 0 and st["partial_checks"] == 0, st
@@ -270,3 +276,35 @@ def test_adaptive_group_size_follows_invalid_share():
         assert sizes[-1] == 16
     finally:
         e.close()
+
+
+def test_level0_pass_and_fall_through():
+    """Level 0 (tbg_config.rlc_batch): a clean batch -- also several callers'
+    batches packed into one launch -- passes the one batch-wide check; one
+    invalid partial anywhere fails it and the group levels return the exact
+    per-item verdicts; the adaptive policy stops running level 0 after an
+    invalid batch."""
+    from charon_amd import engine as eng
+    for cfg in (dict(rlc_batch=eng.RLC_L0_ON, rlc_group=16), dict()):
+        e = eng.Engine(0, **cfg)
+        try:
+            def submit(bs):
+                ts = e.submit_group(eng.OP_VERIFY_AGGREGATE, [
+                    dict(duty_first=b.duty_first, sigs=b.sigs, identifiers=b.identifiers, msgs=(b.msg_data, b.msg_off),
+                         duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold) for b in bs])
+                for b, t in zip(bs, ts):
+                    res = e.collect(t)
+                    assert np.array_equal(res.partial_status == eng.PS_VALID, ~b.injected)
+                    ok = res.duty_status == eng.DS_OK
+                    assert np.array_equal(ok, b.expect_ok)
+                    assert np.array_equal(res.agg[ok], b.group_sig[ok])
+                return e.level0(ts[0])
+            clean = [_make_cluster_batch(e, n, 3, 4, seed=40 + n) for n in (700, 333)]
+            assert submit(clean) == eng.L0_PASSED
+            one_bad = _make_cluster_batch(e, 500, 3, 4, seed=47, inject=0.002)
+            assert one_bad.injected.any()
+            assert submit([clean[0], one_bad]) == eng.L0_FAILED
+            after = submit(clean[1:])
+            assert after == (eng.L0_PASSED if cfg else eng.L0_NOT_RUN)
+        finally:
+            e.close()

@@ -361,3 +361,27 @@ def test_lane_pair_subgroup_check_matches_decode():
     for v in json.load(open(os.path.join(gold, "cfg1_3of4_single.json")))["vectors"]:
         for p in v["partials"]:
             assert L.hc_pair_decode_sig(bytes.fromhex(p["sig"])) == 0
+
+
+def test_level0_bucket_msm_matches_rlc_products():
+    """Level 0's signature side (bls_msm.h, k_msm.hip): the bucket method over
+    the signed base-x digits equals the sum of the per-partial RLC products,
+    including a bucket that meets the same point twice (doubling), a point and
+    its negation cancelling in one bucket, and extreme digit words."""
+    import ctypes
+    L = lib()
+    L.hc_msm_check.restype = ctypes.c_int
+    L.hc_msm_check.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32]
+    sigs = [bls.g2_compress(tb.sign(rng.randrange(1, bls.R), bytes([k]) * 32)) for k in range(6)]
+    neg = bls.g2_compress(bls.g2_neg(bls.g2_decompress(sigs[1])))
+    rs = [rng.getrandbits(64) for _ in range(6)]
+    cases = [
+        (sigs, rs),
+        (sigs[:2] + [sigs[0]], rs[:2] + [rs[0]]),           # same point, same digits: doubling in 4 buckets
+        ([sigs[1], neg, sigs[2]], [rs[1], rs[1], rs[2]]),   # s and -s with the same digits cancel
+        (sigs[:3], [0, 0xFFFF_FFFF_FFFF_FFFF, 0x8000_7FFF_0000_FFFF]),
+    ]
+    for ss, rr in cases:
+        buf = b"".join(ss)
+        arr = (ctypes.c_uint64 * len(rr))(*rr)
+        assert L.hc_msm_check(buf, arr, len(ss)) == 1
