@@ -125,15 +125,18 @@ STAGE_KERNELS = {
 }
 
 
-def stage_mads(wm, args):
-    """Algorithmic u32 mul-adds per launch of each stage for one clean batch
-    (work model of tools/count_work.py: RLC group G = 16, chunk C = 4)."""
+def stage_mads(wm, args, l0=False):
+    """Algorithmic u32 mul-adds per launch of each stage for one clean launch
+    of `merge` batches (work model of tools/count_work.py: RLC group G = 16,
+    chunk C = 4).  l0: the level-0 schedule (k_msm.hip) -- per partial the G1
+    table product and 4 bucket additions, per launch the bucket scalings, tree
+    sums, S's lines, S's Miller quad and one final exponentiation."""
     m = wm["mads"]
     nd, n = args.dvs * max(1, getattr(args, "merge", 1)), args.n  # one launch covers `merge` batches
     np_ = nd * n
     G = wm.get("rlc_schedule", {}).get("group", 16)
     ng = (nd + G - 1) // G
-    return {
+    out = {
         "decode": m["decode_sig"] * np_,
         "hash": m["hash_to_g2"] * nd,
         "combine": m["rlc_partial"] * (np_ - ng) + m["rlc_duty_sum_4"] * nd + m["rlc_group_lines"] * ng,
@@ -141,6 +144,11 @@ def stage_mads(wm, args):
         "verify": m["rlc_check_per_group"] * ng,
         "aggregate": m["aggregate_3of4_all4"] * nd,
     }
+    if l0:
+        out["combine"] = (m["l0_partial"] * np_ + m["l0_duty_sum_4"] * nd + m["l0_bucket_scales"]
+                          + (32768 + 2048 + 128 + 8) * m["g2_add"] + m["lines_h"])
+        out["verify"] = m["l0_per_group"] * ng + m["l0_s_quad"] + m["final_exp_quad"]
+    return out
 
 
 def traffic_model():
@@ -168,7 +176,7 @@ def stage_traffic(tm, stage, batches):
     return int(per_batch * batches)
 
 
-def stage_rooflines(wm, iso, timed, args, value, steps):
+def stage_rooflines(wm, iso, timed, args, value, steps, l0=False):
     """roofline: the dominant stage of the timed region -- its algorithmic
     mul-adds over the timed steps / the summed HIP-event durations of its
     launches (on the slot streams they ran on); with launches in flight
@@ -178,7 +186,8 @@ def stage_rooflines(wm, iso, timed, args, value, steps):
     if not wm or args.t != 3 or args.n != 4:
         return None, None, None
     M = max(1, getattr(args, "merge", 1))
-    per_batch = {k: v / M for k, v in stage_mads(wm, args).items()}
+    per_launch = stage_mads(wm, args, l0)
+    per_batch = {k: v / M for k, v in per_launch.items()}
     tm = traffic_model()
     stage = max(per_batch, key=lambda k: timed.get(k, 0.0))
     total_ms = timed[stage]
@@ -197,13 +206,14 @@ def stage_rooflines(wm, iso, timed, args, value, steps):
                 "frac": round(ach_i / PEAK_MAD_TOPS, 4), "traffic": stage_traffic(tm, iso_stage, M),
                 "algorithmic_mads_per_launch": int(per_batch[iso_stage] * M), "launch_ms": round(iso[iso_stage], 3),
                 "batches_per_launch": M}
-    unit = wm["mads"]["unit_3of4_rlc"]
+    unit = round(sum(per_launch.values()) / (args.dvs * M))  # mul-adds per DV-duty of this schedule
     ach_p = value * unit / 1e12
     pipeline = {"bound": "valu-int-mul", "kernel": "the whole kernel chain (launches in flight together)",
                 "achieved": round(ach_p, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
                 "frac": round(ach_p / PEAK_MAD_TOPS, 4),
                 "traffic": (sum(stage_traffic(tm, s_, 1) or 0 for s_ in STAGE_KERNELS) or None) if tm else None,
-                "work_per_unit_mads": unit,
+                "work_per_unit_mads": unit, "schedule": "level 0 (batch-wide check, bucket MSM)" if l0 else
+                "level-1 groups",
                 "reference_schedule_mads_per_unit": wm["mads"]["unit_3of4_single_lane_schedule"],
                 "reference_schedule_equivalent_tmads": round(value * wm["mads"]["unit_3of4_single_lane_schedule"] / 1e12, 3)}
     return roofline, isolated, pipeline
@@ -371,6 +381,7 @@ def main():
     b = batches[0][0]
     flat = [x for g in batches for x in g]
     group_used = e.stats(tickets[0])["group_size"]  # before api_pipeline reuses the slots (tickets expire)
+    l0_state = e.level0(tickets[0])
 
     units = args.dvs * args.steps * ws
     value = units / elapsed
@@ -382,7 +393,7 @@ def main():
     iso = e.replay(tickets[0], 1)
     # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
     roofline, roofline_isolated, roofline_pipeline = stage_rooflines(work_model(), iso, kernel_ms, args, value / ws,
-                                                                     args.steps)
+                                                                     args.steps, l0=l0_state == eng.L0_PASSED)
     # (reuses the engine's slots: after the replays and the isolated pass)
     api = api_pipeline(e, eng, flat, args.inflight, args.api_batches, M) if args.api_batches else None
 
@@ -398,6 +409,7 @@ def main():
                    "partials_per_step_per_gpu": args.dvs * args.n, "parallelism": f"shard{ws}",
                    "inflight_launches": args.inflight, "batches_per_launch": M,
                    "rlc_group": group_used,
+                   "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),

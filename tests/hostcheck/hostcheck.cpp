@@ -563,3 +563,57 @@ int hc_msm_check(const uint8_t* sigs96, const uint64_t* r, uint32_t n) {
   return jac_eq(got, ref) ? 1 : 0;
 }
 }  // extern "C"
+
+// Level-0 stages (tools/count_work.py): one partial's G1 product from the
+// key's pair table plus its 4 bucket additions; the G1-only duty sum; one
+// bucket's [2j + 1]; one tree addition.
+extern "C" {
+void hc_stage_l0_partial(uint64_t r64) {
+  G1A ap, am;
+  rlc_pair_from_inv(g_pk, g_xpk, fp_inv(fp_reduce(fp_sub(g_xpk.x, g_pk.x))), ap, am);  // at key load
+  G2J acc = jac_dbl(jac_from_aff(g_sig));
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  uint32_t u[4];
+  rlc_digits(r64, u);
+  G1J P = rlc_mul_table(ap, am, fp_from_const(G1_BETA), u);
+  (void)P;
+  for (uint32_t k = 0; k < 4; ++k) {
+    bool neg;
+    (void)msm_bucket(u[k], neg);
+    G2A p = msm_psi_k(g_sig, k);
+    if (neg) p.y = fp2_reduce(fp2_neg(p.y));
+    acc = jac_add_aff_in(acc, p);
+  }
+}
+void hc_stage_duty_sum_p(int n) {
+  G1J P = jac_from_aff(g_pk), P1 = jac_dbl(P);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  G1J accP = P;
+  for (int k = 1; k < n; ++k) accP = jac_add(accP, P1);
+  G1A a;
+  jac_to_aff(accP, a);
+}
+void hc_stage_l0_bucket_scale(uint32_t m) {
+  G2J b = jac_dbl(jac_from_aff(g_sig));
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  G2J acc = b;
+  const int top = 31 - __builtin_clz(m);
+  for (int bit = top - 1; bit >= 0; --bit) {
+    acc = jac_dbl_in(acc);
+    if ((m >> bit) & 1u) acc = jac_add_in<Fp2, true>(acc, b);
+  }
+}
+void hc_stage_g2_add(void) {
+  G2J a = jac_dbl(jac_from_aff(g_sig)), b = jac_dbl(a);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  a = jac_add_in<Fp2, true>(a, b);
+}
+}  // extern "C"

@@ -72,6 +72,30 @@ def main():
     chunk2f, _ = measure(lib.hc_stage_miller_chunk, C, 1)
     final4, _ = measure(lib.hc_stage_group_final, G // C)
     rlc_check_per_group = chunk2f + (G // C - 1) * chunk2 + final4
+    # Level 0 (k_msm.hip): per partial the G1 table product and 4 bucket
+    # additions; per duty the G1-only sum; per group its P chunks and the
+    # products folding them (nch quad products, tree included); per launch
+    # the bucket scalings (sampled over j), the tree sums, S's lines, S's
+    # Miller quad and ONE final exponentiation.
+    for fn in ("hc_stage_l0_partial", "hc_stage_duty_sum_p", "hc_stage_l0_bucket_scale", "hc_stage_g2_add"):
+        getattr(lib, fn).restype = None
+    lib.hc_stage_l0_partial.argtypes = [ctypes.c_uint64]
+    lib.hc_stage_l0_bucket_scale.argtypes = [ctypes.c_uint32]
+    l0_partial, _ = measure(lib.hc_stage_l0_partial, 0x9E3779B97F4A7C15)
+    duty_sum_p4, _ = measure(lib.hc_stage_duty_sum_p, 4)
+    step = 61
+    scale_sample = [measure(lib.hc_stage_l0_bucket_scale, 2 * j + 1)[0] for j in range(0, 32768, step)]
+    bucket_scales = sum(scale_sample) * 32768 / len(scale_sample)
+    g2_add, _ = measure(lib.hc_stage_g2_add)
+    final1, _ = measure(lib.hc_stage_group_final, 1)
+    qmul = measure(lib.hc_stage_group_final, 2)[0] - final1
+    s_quad, _ = measure(lib.hc_stage_miller_chunk, 0, 1)
+    nch = G // C
+    l0_per_group = nch * chunk2 + nch * qmul
+    l0_per_launch = bucket_scales + (32768 + 2048 + 128 + 8) * g2_add + lines_h + s_quad + final1
+    launch_dvs = 16 * 10000  # bench default: 16 batches of 10k DVs per launch
+    unit_3of4_l0 = (4 * decode + hash_ + lines_h + 4 * l0_partial + duty_sum_p4 + l0_per_group / G + agg
+                    + l0_per_launch / launch_dvs)
     # every candidate but the first of each group is randomised: (4 G - 1) / G per duty
     unit_3of4_rlc = (4 * decode + hash_ + lines_h + (4 * G - 1) / G * rlc_partial + duty_sum4 + group_lines8 / G
                      + rlc_check_per_group / G + agg)
@@ -87,6 +111,10 @@ def main():
                  "rlc_miller_chunk": chunk2, "rlc_miller_chunk_folded": chunk2f, "rlc_group_final": final4,
                  "rlc_check_per_group": rlc_check_per_group,
                  "aggregate_3of4_all4": agg,
+                 "l0_partial": l0_partial, "l0_duty_sum_4": duty_sum_p4, "l0_per_group": l0_per_group,
+                 "l0_per_launch": round(l0_per_launch), "l0_bucket_scales": round(bucket_scales),
+                 "g2_add": g2_add, "quad_mul": qmul, "l0_s_quad": s_quad, "final_exp_quad": final1,
+                 "unit_3of4_l0": round(unit_3of4_l0), "l0_launch_dvs": launch_dvs,
                  "unit_3of4_rlc": round(unit_3of4_rlc), "unit_3of4_each": unit_3of4,
                  "unit_3of4_single_lane_schedule": unit_3of4_v1},
         "fp_mul_equiv": {k: round(v / 392, 1) for k, v in
@@ -95,7 +123,9 @@ def main():
                           "rlc_partial": rlc_partial, "rlc_duty_sum_4": duty_sum4,
                           "rlc_group_lines": group_lines8, "rlc_miller_chunk": chunk2,
                           "rlc_miller_chunk_folded": chunk2f, "rlc_group_final": final4,
-                          "aggregate_3of4_all4": agg, "unit_3of4_rlc": unit_3of4_rlc,
+                          "aggregate_3of4_all4": agg, "l0_partial": l0_partial, "l0_duty_sum_4": duty_sum_p4,
+                          "l0_per_group": l0_per_group, "l0_per_launch": l0_per_launch,
+                          "unit_3of4_l0": unit_3of4_l0, "unit_3of4_rlc": unit_3of4_rlc,
                           "unit_3of4_each": unit_3of4, "unit_3of4_reference_schedule": unit_3of4_v1}.items()},
         "verify_hbm_bytes_per_launch": None,
     }
