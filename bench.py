@@ -288,6 +288,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=3, help="engine slots replayed round-robin (launches in flight)")
     ap.add_argument("--merge", type=int, default=16,
                     help="10k-DV batches per slot, submitted together as one device batch (tbg_submit_group)")
+    ap.add_argument("--launches", type=int, default=0,
+                    help="spread the timed steps over at least this many launches (default: one per slot)")
     ap.add_argument("--verify-mode", type=int, default=0, help="0 = RLC groups with fallback, 1 = per-partial checks")
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
@@ -356,7 +358,7 @@ def main():
         round-robin over the slots (a prefix of a packed device batch is a
         batch of its own), so a short run still has `inflight` launches
         overlapping instead of a full launch plus a small remainder."""
-        L = max(-(-n // M), min(len(tickets), n))
+        L = max(-(-n // M), min(len(tickets), n), min(args.launches, n))
         base, extra = divmod(n, L)
         ts, ps = [], []
         for k in range(L):

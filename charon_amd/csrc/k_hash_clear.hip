@@ -1,27 +1,75 @@
-// Cofactor clearing of hash_to_G2 (the middle kernel of k_hash.hip's chain),
-// in its own translation unit: device functions shared with the two-wave
-// kernels of k_hash.hip would otherwise be compiled for this kernel's
-// unconstrained register budget, and a kernel inherits its callees' count
-// (k_hash_map dropped to one wave per SIMD that way).
+// Cofactor clearing of hash_to_G2 (the middle of k_hash.hip's chain),
+// Budroni-Pintore (RFC 9380 G.3):
+//   h(P) = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P)
+//        = [x]([x]P + psi(P)) + psi^2(2P) - psi(P) - [x]P - P,
+// in three lane-PAIR kernels (bls_pair.h: the Fp2 coordinates split over two
+// lanes) so each holds at most two G2 points across its [x] loop and runs two
+// waves per SIMD:
+//   k_hash_clear_x1   t1 = [x]P, u = t1 + psi(P)      (temporaries in h_jac)
+//   k_hash_clear_x2   v = [x]u
+//   k_hash_clear_fin  h = psi^2(2P) - psi(P) + v - t1 - P
+// The single-lane form kept three live points across the second [x] loop and
+// ran at one wave per SIMD (12.3 ms per 160k-message launch); it is kept as
+// the host reference (g2_clear_cofactor_t, bls_curve.h) the tests check.
 #define TBG_ADD_DBL_INLINE 1
+#ifndef TBG_SCHED_FENCE
+#define TBG_SCHED_FENCE 1  // products in program order: fits the pair kernels in 256 VGPRs (bls_field.h)
+#endif
 #include "tbls_launch.h"
 #include "bls_h2c.h"
+#include "bls_pair.h"
 
 namespace tbg {
 
-// Cofactor clearing stays one lane per message at one wave per SIMD: its
-// live state (three G2 points across the second [x] multiplication) does
-// not fit 256 VGPRs even split over a lane pair (measured: 1,271 spilled
-// VGPRs for the pair form, tools notes in DESIGN.md).  Splitting it off is
-// what lets k_hash_map run at two waves per SIMD.
-__global__ void TBG_LAUNCH k_hash_clear(DevBatch B) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ Jac<Fp2x> px_psi(const Jac<Fp2x>& p) {
+  return {f_mulc(f_conj(p.X), PSI_X), f_mulc(f_conj(p.Y), PSI_Y), f_reduce(f_conj(p.Z))};
+}
+
+// [x] p = -[|x|] p (63 doublings, 5 additions; the P == Q case doubles inline)
+__device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
+  Jac<Fp2x> acc = p;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    acc = jac_dbl_in(acc);
+    if ((X_ABS >> i) & 1) acc = jac_add_in<Fp2x, true>(acc, p);
+  }
+  return jac_neg(acc);
+}
+
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x1(DevBatch B) {
+  const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (m >= B.n_msgs) return;
-  B.h_jac[m] = g2_clear_cofactor_t<true>(B.h_jac[m]);
+  const Jac<Fp2x> p = px_load(B.h_jac[m]);
+  const Jac<Fp2x> t1 = px_mul_x(p);
+  px_store(B.h_jac[B.n_msgs + m], t1);
+  px_store(B.h_jac[2 * B.n_msgs + m], jac_add_in<Fp2x, true>(t1, px_psi(p)));
+}
+
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x2(DevBatch B) {
+  const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (m >= B.n_msgs) return;
+  G2J* u = B.h_jac + 2 * B.n_msgs + m;
+  px_store(*u, px_mul_x(px_load(*u)));
+}
+
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_fin(DevBatch B) {
+  const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (m >= B.n_msgs) return;
+  const Jac<Fp2x> p = px_load(B.h_jac[m]);
+  const Jac<Fp2x> psi_p = px_psi(p);
+  Jac<Fp2x> t3 = px_psi(px_psi(jac_dbl_in(p)));                       // psi^2(2P)
+  t3 = jac_add_in<Fp2x, true>(t3, jac_neg(psi_p));                    // - psi(P)
+  t3 = jac_add_in<Fp2x, true>(t3, px_load(B.h_jac[2 * B.n_msgs + m]));  // + [x]([x]P + psi(P))
+  t3 = jac_add_in<Fp2x, true>(t3, jac_neg(px_load(B.h_jac[B.n_msgs + m])));  // - [x]P
+  px_store(B.h_jac[m], jac_add_in<Fp2x, true>(t3, jac_neg(p)));      // - P
 }
 
 void launch_hash_clear(const DevBatch& B, hipStream_t st) {
-  if (B.n_msgs) TBG_KLAUNCH(k_hash_clear, grid_for(B.n_msgs), dim3(kBlock), st, B);
+  if (!B.n_msgs) return;
+  const dim3 grid = grid_for(2 * B.n_msgs);
+  TBG_KLAUNCH(k_hash_clear_x1, grid, dim3(kBlock), st, B);
+  TBG_KLAUNCH(k_hash_clear_x2, grid, dim3(kBlock), st, B);
+  TBG_KLAUNCH(k_hash_clear_fin, grid, dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

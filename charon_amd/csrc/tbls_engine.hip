@@ -430,7 +430,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_sig_aff = sec(sizeof(G2A) * (size_t)np);
   size_t w_h_aff = sec(sizeof(G2A) * (size_t)nm);
   size_t w_h_st = sec(4ull * nm);
-  size_t w_h_jac = sec(sizeof(G2J) * (size_t)nm);
+  size_t w_h_jac = sec(3 * sizeof(G2J) * (size_t)nm);  // H(m) + the cofactor clearing's two temporaries
   size_t w_lam = sec(32ull * np);
   size_t w_sl = sec(verify ? 4ull * LINES_WORDS * np : 0);
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
@@ -872,7 +872,7 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
   size_t mb = msg_off[n_msgs];
   size_t need = align_up(32ull * n, 16) + align_up(mb + 1, 16) + align_up(4ull * (n_msgs + 1), 16) + align_up(4ull * n, 16) +
                 align_up(sizeof(G2A) * (size_t)n_msgs, 16) + align_up(4ull * n_msgs, 16) + align_up(96ull * n, 16) +
-                align_up(sizeof(G2J) * (size_t)n_msgs, 16);
+                align_up(3 * sizeof(G2J) * (size_t)n_msgs, 16);
   uint8_t* base = nullptr;
   if (hipMalloc(&base, need) != hipSuccess) return TBG_E_OOM;
   size_t o = 0;
@@ -884,7 +884,7 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
   G2A* d_h = (G2A*)sec(sizeof(G2A) * (size_t)n_msgs);
   int32_t* d_hs = (int32_t*)sec(4ull * n_msgs);
   uint8_t* d_sig = sec(96ull * n);
-  G2J* d_hj = (G2J*)sec(sizeof(G2J) * (size_t)n_msgs);
+  G2J* d_hj = (G2J*)sec(3 * sizeof(G2J) * (size_t)n_msgs);
   int rc = TBG_OK;
   hipStream_t st = c->stream;
   if (hipMemcpyAsync(d_sk, sk32, 32ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -1057,7 +1057,7 @@ int tbg_fast_aggregate_verify(tbg_ctx* c, const uint32_t* pubkey_ids, const uint
   int rc = a.alloc(SumHost::bytes(n, h.n_chunks(), sizeof(G1J)) + align_up(4ull * nk + 4, 16) +
                    align_up(48ull * n, 16) * 2 + align_up(sizeof(G1A) * n, 16) * 2 + align_up(4ull * n, 16) * 6 +
                    align_up(mb + 1, 16) + align_up(4ull * (n + 1), 16) * 2 + align_up(96ull * n, 16) + align_up(n, 16) +
-                   align_up(sizeof(G2A) * n, 16) * 2 + align_up(sizeof(G2J) * n, 16) + 2 * align_up(lines, 16) +
+                   align_up(sizeof(G2A) * n, 16) * 2 + align_up(3 * sizeof(G2J) * n, 16) + 2 * align_up(lines, 16) +
                    align_up(4ull * tbg::CNT_WORDS, 16));
   if (rc != TBG_OK) return rc;
   hipStream_t st = c->stream;
@@ -1092,7 +1092,7 @@ int tbg_fast_aggregate_verify(tbg_ctx* c, const uint32_t* pubkey_ids, const uint
   B.sig_aff = (G2A*)a.sec(sizeof(G2A) * n);
   B.h_aff = (G2A*)a.sec(sizeof(G2A) * n);
   B.h_status = (int32_t*)a.sec(4ull * n);
-  B.h_jac = (G2J*)a.sec(sizeof(G2J) * n);
+  B.h_jac = (G2J*)a.sec(3 * sizeof(G2J) * n);
   B.sig_lines = (uint32_t*)a.sec(lines);
   B.h_lines = (uint32_t*)a.sec(lines);
   B.counters = (uint32_t*)a.sec(4ull * tbg::CNT_WORDS);

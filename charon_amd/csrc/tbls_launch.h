@@ -49,7 +49,8 @@ struct DevBatch {
   G2A* sig_aff;
   G2A* h_aff;
   int32_t* h_status;
-  G2J* h_jac;          // [n_msgs] H(m) before affine conversion (k_hash_map / _clear / _affine)
+  G2J* h_jac;          // [3 n_msgs] H(m) before affine conversion (k_hash_map / _clear / _affine), then
+                       // the cofactor clearing's temporaries [x]P and [x]P + psi(P) (k_hash_clear.hip)
   uint32_t* lam;       // [n_partials][8] scalar words
   uint32_t* sig_lines;  // [n_partials][LINES_WORDS] Miller lines of listed signatures (-g1 folded in)
   uint32_t* h_lines;    // [n_msgs][LINES_WORDS] Miller lines of each H(m) (G1 factor left out)
