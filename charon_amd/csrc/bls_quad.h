@@ -6,8 +6,8 @@
 //   A0 = (a_0, a_3) = (c0.c0, c1.c1)
 //   A1 = (a_1, a_4) = (c1.c0, c0.c2)
 //   A2 = (a_2, a_5) = (c0.c1, c1.c2)
-// Lane q = lane % 4 of a quad owns A_q (q = 0, 1, 2; lane 3 mirrors lane 2 and
-// its results are ignored).  A product is Karatsuba-3 over Fp4: every lane
+// Lane q = 0, 1, 2 of a lane group (the "quad": a trio of lanes of a DPP row
+// by default, see TBG_TRIO below) owns A_q.  A product is Karatsuba-3 over Fp4: every lane
 // computes two Fp4 products (6 Fp2 products) instead of one lane computing
 // 18, and operands / partial products move between the lanes of the quad
 // with DPP quad_perm moves (full-rate VALU, no LDS).  The per-lane pieces
@@ -127,32 +127,81 @@ namespace tbg {
 #define TBG_QUAD_FN __noinline__
 #endif
 
-// quad_perm controls (lane q reads lane sel[q]); lane 3 behaves as lane 2.
-constexpr int QP_NEXT = 1 | (2 << 2) | (0 << 4) | (0 << 6);  // (q + 1) mod 3
-constexpr int QP_PREV = 2 | (0 << 2) | (1 << 4) | (1 << 6);  // (q + 2) mod 3
-constexpr int QP_SW12 = 0 | (2 << 2) | (1 << 4) | (1 << 6);  // {0, 2, 1}
-constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA;      // broadcast lane 0 / 1 / 2
+// Lane groups.  TBG_TRIO = 1 (default): an Fp12 lives on a TRIO of
+// consecutive lanes of a 16-lane DPP row -- 5 trios per row, lane 15 idle,
+// so 60 of 64 lanes work; operands move with DPP row shifts (two per word
+// plus a select).  TBG_TRIO = 0: the quad layout (lanes 4k .. 4k + 3, lane 3
+// mirrors lane 2: 48 of 64 lanes work) with one quad_perm move per word.
+#ifndef TBG_TRIO
+#define TBG_TRIO 1
+#endif
+// exchange kinds: lane q of the group reads the value of lane ...
+enum QuadXch : int {
+  QP_NEXT = 0,  // (q + 1) mod 3
+  QP_PREV = 1,  // (q + 2) mod 3
+  QP_SW12 = 2,  // {0, 2, 1}[q]
+  QP_B0 = 3,    // 0 (broadcast)
+  QP_B1 = 4,    // 1
+  QP_B2 = 5,    // 2
+};
 
 template <int CTRL>
 TBG_DEV uint32_t dpp_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
 }
-template <int CTRL>
-TBG_DEV Fp xch(const Fp& x) {
-  Fp r;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) r.l[i] = dpp_u32<CTRL>(x.l[i]);
-  return r;
-}
-template <int CTRL>
-TBG_DEV Fp2 xch(const Fp2& x) { return {xch<CTRL>(x.c0), xch<CTRL>(x.c1)}; }
-template <int CTRL>
-TBG_DEV Fp4 xch(const Fp4& x) { return {xch<CTRL>(x.a), xch<CTRL>(x.b)}; }
 
+#if TBG_TRIO
+// DPP row shifts: row_shl:n -- lane l reads lane l + n of its row; row_shr:n -- lane l - n.
+constexpr int DPP_SHL1 = 0x101, DPP_SHL2 = 0x102, DPP_SHR1 = 0x111, DPP_SHR2 = 0x112;
+TBG_DEV int quad_lane() { return (int)((threadIdx.x & 15u) % 3u); }
+// Fp12 slot of global thread t (UINT32_MAX for the idle lane 15 of a row),
+// and the threads n slots need.
+TBG_HD inline uint32_t fp12_slot(uint32_t t) {
+  const uint32_t l = t & 15u;
+  return l == 15u ? 0xFFFFFFFFu : (t >> 4) * 5u + l / 3u;
+}
+inline uint32_t fp12_threads(uint32_t n) { return 16u * ((n + 4u) / 5u); }
+template <int K>
+TBG_DEV uint32_t xch_u32(uint32_t v) {
+  const int q = quad_lane();
+  if (K == QP_NEXT) { const uint32_t a = dpp_u32<DPP_SHL1>(v), b = dpp_u32<DPP_SHR2>(v); return q < 2 ? a : b; }
+  if (K == QP_PREV) { const uint32_t a = dpp_u32<DPP_SHL2>(v), b = dpp_u32<DPP_SHR1>(v); return q == 0 ? a : b; }
+  if (K == QP_SW12) { const uint32_t a = dpp_u32<DPP_SHL1>(v), b = dpp_u32<DPP_SHR1>(v); return q == 0 ? v : (q == 1 ? a : b); }
+  if (K == QP_B0) { const uint32_t a = dpp_u32<DPP_SHR1>(v), b = dpp_u32<DPP_SHR2>(v); return q == 0 ? v : (q == 1 ? a : b); }
+  if (K == QP_B1) { const uint32_t a = dpp_u32<DPP_SHL1>(v), b = dpp_u32<DPP_SHR1>(v); return q == 0 ? a : (q == 1 ? v : b); }
+  const uint32_t a = dpp_u32<DPP_SHL2>(v), b = dpp_u32<DPP_SHL1>(v);  // QP_B2
+  return q == 0 ? a : (q == 1 ? b : v);
+}
+#else
+// quad_perm controls (lane q reads lane sel[q]); lane 3 behaves as lane 2.
+constexpr int QPERM[6] = {
+    1 | (2 << 2) | (0 << 4) | (0 << 6),  // NEXT
+    2 | (0 << 2) | (1 << 4) | (1 << 6),  // PREV
+    0 | (2 << 2) | (1 << 4) | (1 << 6),  // SW12
+    0x00, 0x55, 0xAA};                   // broadcast lane 0 / 1 / 2
 TBG_DEV int quad_lane() {
   int q = (int)(threadIdx.x & 3);
   return q > 2 ? 2 : q;
 }
+TBG_HD inline uint32_t fp12_slot(uint32_t t) { return t >> 2; }
+inline uint32_t fp12_threads(uint32_t n) { return 4u * n; }
+template <int K>
+TBG_DEV uint32_t xch_u32(uint32_t v) { return dpp_u32<QPERM[K]>(v); }
+#endif
+// lane 0 of this thread's group (the list-slot owner of push_ident)
+TBG_DEV uint32_t quad_lead_lane() { return threadIdx.x - (uint32_t)quad_lane(); }
+
+template <int K>
+TBG_DEV Fp xch(const Fp& x) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = xch_u32<K>(x.l[i]);
+  return r;
+}
+template <int K>
+TBG_DEV Fp2 xch(const Fp2& x) { return {xch<K>(x.c0), xch<K>(x.c1)}; }
+template <int K>
+TBG_DEV Fp4 xch(const Fp4& x) { return {xch<K>(x.a), xch<K>(x.b)}; }
 
 // C = A * B (both quad-distributed).  The _in bodies are for kernel loops;
 // the out-of-line forms serve the final exponentiation's callable loops.
@@ -263,7 +312,7 @@ TBG_DEV bool quad_is_one(const Fp4& A) {
   int q = quad_lane();
   bool ok = fp2_is_zero(A.b) && (q == 0 ? fp2_eq(A.a, fp2_one()) : fp2_is_zero(A.a));
   uint32_t v = ok ? 1u : 0u;
-  return (dpp_u32<QP_B0>(v) & dpp_u32<QP_B1>(v) & dpp_u32<QP_B2>(v)) != 0;
+  return (xch_u32<QP_B0>(v) & xch_u32<QP_B1>(v) & xch_u32<QP_B2>(v)) != 0;
 }
 
 }  // namespace tbg

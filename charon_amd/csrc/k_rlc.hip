@@ -21,7 +21,8 @@
 // duty, a bad duty to its bad partial; whatever the exponent tests cannot
 // pin down (two or more bad members) goes to level 3, the exact per-item
 // check -- so every partial's verdict is the one tbls.Verify would return.
-// One quad of lanes runs each product check (bls_quad.h) over Miller lines
+// One lane group (a "quad": a trio of lanes of a DPP row, bls_quad.h) runs
+// each product check over Miller lines
 // stored in HBM: the H(m) lines are shared by all partials of a message, the
 // -g1 factor is folded into the lines of S / S_c / s_i.  Work lists of the
 // fallback levels are compacted on the device (atomic counters), so a clean
@@ -128,7 +129,7 @@ __global__ void TBG_LAUNCH k_rlc_group_lines(DevBatch B) {
 template <bool INL = false>
 __device__ __forceinline__ Fp4 quad_line_at(const Fp4& f, const uint32_t* lines, int idx, const Fp& nx, const Fp& y) {
   const uint32_t* src = lines + LINE_WORDS * idx;
-  const bool first = (threadIdx.x & 3) == 0;
+  const bool first = quad_lane() == 0;
   Fp2 l0, lk;
   for (int i = 0; i < NL; ++i) {
     l0.c0.l[i] = src[i];
@@ -149,7 +150,7 @@ __device__ __forceinline__ Fp4 quad_line_folded(const Fp4& f, const uint32_t* li
 constexpr int QUAD_WORDS = 4 * NL;
 __device__ __forceinline__ void quad_store(uint32_t* dst, const Fp4& A) {
   int q = quad_lane();
-  if ((threadIdx.x & 3) == 3) return;
+  if (TBG_TRIO == 0 && (threadIdx.x & 3) == 3) return;  // the quad layout's mirror lane
   const Fp* f[4] = {&A.a.c0, &A.a.c1, &A.b.c0, &A.b.c1};
   for (int k = 0; k < 4; ++k)
     for (int j = 0; j < NL; ++j) dst[QUAD_WORDS * q + k * NL + j] = f[k]->l[j];
@@ -181,7 +182,7 @@ __global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B, in
   // P chunks first, then the S quads: S quads evaluate one line per step
   // instead of C, and in waves of their own they finish early instead of
   // each holding a P chunk's wave slot for its full length
-  uint32_t qd = t >> 2;
+  uint32_t qd = fp12_slot(t);
   const uint32_t np_q = n_groups * nch;
   uint32_t g, c;
   bool l0_s = false;
@@ -244,9 +245,9 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
   uint32_t nq = (G + C - 1) / C + 1;
-  uint32_t g = t >> 2;
+  uint32_t g = fp12_slot(t);
   if (g >= n_groups) return;
-  const bool lead = (t & 3) == 0;
+  const bool lead = quad_lane() == 0;
   if (B.grp_state[g] != GRP_LINES) return;  // empty groups have nothing to resolve; GRP_FAIL stays failed
   uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
   for (uint32_t d = d0; d < d1; ++d) {
@@ -270,12 +271,12 @@ __global__ void TBG_LAUNCH k_l0_fold(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk;
   const uint32_t n_groups = (B.n_duties + G - 1) / G, nch = (G + C - 1) / C, nq = nch + 1;
-  const uint32_t g = t >> 2;
+  const uint32_t g = fp12_slot(t);
   if (g >= n_groups || B.counters[CNT_L0_BAD]) return;
   const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
   for (uint32_t d = d0; d < d1; ++d) {
     if (B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] != 0) {
-      if ((t & 3) == 0) B.counters[CNT_L0_BAD] = 1;
+      if (quad_lane() == 0) B.counters[CNT_L0_BAD] = 1;
       return;
     }
   }
@@ -288,7 +289,7 @@ __global__ void TBG_LAUNCH k_l0_fold(DevBatch B) {
 // Product tree, one quad per L0_TREE_FAN values of grp_f[in .. in + n).
 __global__ void TBG_LAUNCH k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32_t out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t q = t >> 2, a0 = q * L0_TREE_FAN;
+  const uint32_t q = fp12_slot(t), a0 = q * L0_TREE_FAN;
   if (a0 >= n || B.counters[CNT_L0_BAD]) return;
   const uint32_t a1 = min(a0 + L0_TREE_FAN, n);
   Fp4 f = quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a0));
@@ -299,7 +300,7 @@ __global__ void TBG_LAUNCH k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32
 // One quad: the last <= L0_TREE_FAN values times the S pair's product, one
 // final exponentiation for the whole batch.
 __global__ void TBG_LAUNCH k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
-  if (threadIdx.x >= 4 || B.counters[CNT_L0_BAD]) return;
+  if (fp12_slot(threadIdx.x) != 0 || B.counters[CNT_L0_BAD]) return;
   Fp4 f = quad_load(B.batch_f);
   for (uint32_t a = 0; a < n; ++a) f = quad_mul(f, quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
   f = quad_final_exp_in(quad_conj(f));
@@ -419,7 +420,7 @@ __device__ __forceinline__ void push_ident(const DevBatch& B, uint32_t d, const 
     slot = atomicAdd(&B.counters[CNT_DUTIES], 1u);
     B.id_list[slot] = d;
   }
-  slot = (uint32_t)__shfl((int)slot, (int)(threadIdx.x & ~3u));
+  slot = (uint32_t)__shfl((int)slot, (int)quad_lead_lane());
   quad_store(B.id_fe + (size_t)3 * QUAD_WORDS * slot, A);
 }
 // A duty known to be bad: one candidate -> that partial is invalid (the check
@@ -435,9 +436,9 @@ __device__ __forceinline__ void resolve_bad_duty(const DevBatch& B, uint32_t d, 
 // go to level 1.5b with the chunk's value (a degenerate S_c: level 3).
 __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = t >> 2;
+  uint32_t k = fp12_slot(t);
   if (k >= B.counters[CNT_CHUNKS]) return;
-  const bool lead = (t & 3) == 0;
+  const bool lead = quad_lane() == 0;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C, nq = nch + 1;
   const uint32_t entry = B.chunk_list[k], qc = entry & ~CHUNK_DEGENERATE, g = qc / nch, c = qc % nch;
   const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
@@ -511,9 +512,9 @@ __global__ void TBG_LAUNCH k_rlc_cident_lines(DevBatch B) {
 // chunk's candidates go to level 3.
 __global__ void TBG_LAUNCH k_rlc_cident_check(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t j = t >> 2;
+  uint32_t j = fp12_slot(t);
   if (j >= B.counters[CNT_CID]) return;
-  const bool lead = (t & 3) == 0;
+  const bool lead = quad_lane() == 0;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C;
   const uint32_t entry = B.cid_list[j], k = entry & ~ID_DEGENERATE;
   const uint32_t qc = B.chunk_list[k], g = qc / nch, c = qc % nch;
@@ -591,9 +592,9 @@ __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
 // Found -> partial w invalid, the others valid; not found -> level 3.
 __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = t >> 2;
+  uint32_t k = fp12_slot(t);
   if (k >= B.counters[CNT_DUTIES]) return;
-  const bool lead = (t & 3) == 0;
+  const bool lead = quad_lane() == 0;
   const uint32_t entry = B.id_list[k], d = entry & ~ID_DEGENERATE;
   uint32_t found = 0;
   if (!(entry & ID_DEGENERATE)) {
@@ -660,9 +661,9 @@ __global__ void TBG_LAUNCH k_lines_sig_list(DevBatch B) {
 // Level 3 check: one quad per listed partial, the exact CoreVerify.
 __global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = t >> 2;
+  uint32_t k = fp12_slot(t);
   if (k >= B.counters[CNT_PARTIALS]) return;
-  const bool lead = (t & 3) == 0;
+  const bool lead = quad_lane() == 0;
   uint32_t i = B.part_list[k];
   uint32_t m = B.duty_msg[B.partial_duty[i]];
   if (B.h_status[m] != 0) {
@@ -716,12 +717,12 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
     if (B.rlc_batch) {
       // level 0: the P chunks (kept for the group levels) and S, one product
-      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * (n_groups * nch + 1)), dim3(kBlock), st, B, (int)MILLER_L0);
-      TBG_KLAUNCH(k_l0_fold, grid_for(4 * n_groups), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(fp12_threads((n_groups * nch + 1))), dim3(kBlock), st, B, (int)MILLER_L0);
+      TBG_KLAUNCH(k_l0_fold, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
       uint32_t in = 0, n = n_groups, out = n_groups;
       while (n > L0_TREE_FAN) {
         const uint32_t m = (n + L0_TREE_FAN - 1) / L0_TREE_FAN;
-        TBG_KLAUNCH(k_l0_tree, grid_for(4 * m), dim3(kBlock), st, B, in, n, out);
+        TBG_KLAUNCH(k_l0_tree, grid_for(fp12_threads(m)), dim3(kBlock), st, B, in, n, out);
         in = out;
         out += m;
         n = m;
@@ -734,27 +735,27 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
       TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B, (int)DSUM_FALLBACK_S);
       TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
       launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
-      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups), dim3(kBlock), st, B, (int)MILLER_GROUP_S);
+      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B, (int)MILLER_GROUP_S);
     } else {
-      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(4 * n_groups * (nch + 1)), dim3(kBlock), st, B, (int)MILLER_GROUPS);
+      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(fp12_threads(n_groups * (nch + 1))), dim3(kBlock), st, B, (int)MILLER_GROUPS);
     }
-    TBG_KLAUNCH(k_rlc_group_final, grid_for(4 * n_groups), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_rlc_group_final, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
       TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
       launch_lines_fold(B, FOLD_CHUNKS, n_groups * nch, st);
-      TBG_KLAUNCH(k_rlc_check_chunks, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_check_chunks, grid_for(fp12_threads(n_groups * nch)), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_cident_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
       launch_lines_fold(B, FOLD_CID, n_groups * nch, st);
-      TBG_KLAUNCH(k_rlc_cident_check, grid_for(4 * n_groups * nch), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_cident_check, grid_for(fp12_threads(n_groups * nch)), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_rlc_ident_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
       launch_lines_fold(B, FOLD_IDENT, B.n_duties, st);
-      TBG_KLAUNCH(k_rlc_ident_check, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_rlc_ident_check, grid_for(fp12_threads(B.n_duties)), dim3(kBlock), st, B);
     }
   }
   if (B.n_partials) {
     TBG_KLAUNCH(k_lines_sig_list, grid_for(B.n_partials), dim3(kBlock), st, B);
-    TBG_KLAUNCH(k_verify_list, grid_for(4 * B.n_partials), dim3(kBlock), st, B, pk_aff);
+    TBG_KLAUNCH(k_verify_list, grid_for(fp12_threads(B.n_partials)), dim3(kBlock), st, B, pk_aff);
   }
 }
 
