@@ -115,11 +115,13 @@ def work_model():
 # Stages of the kernel chain (tbg_last_timings order) and their kernels.
 STAGE_KERNELS = {
     "decode": ["k_decode_sigs", "k_subgroup_sigs"],
-    "hash": ["k_hash_map", "k_hash_clear", "k_hash_affine"],
-    "combine": ["k_rlc_partial2", "k_rlc_duty_sum", "k_rlc_group_lines"],
+    "hash": ["k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
+    "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_sum", "k_msm_scan", "k_msm_scatter", "k_rlc_duty_sum",
+                "k_lines_fold<4>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<0>"],
     "h_lines": ["k_lines_h"],
-    "verify": ["k_rlc_miller_chunks", "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_chunk_lines",
-               "k_rlc_check_chunks", "k_rlc_cident_lines", "k_rlc_cident_check", "k_rlc_ident_lines",
+    "verify": ["k_rlc_miller_chunks", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after", "k_rlc_group_final",
+               "k_rlc_resolve_groups", "k_rlc_chunk_lines", "k_lines_fold<1>", "k_rlc_check_chunks",
+               "k_rlc_cident_lines", "k_lines_fold<2>", "k_rlc_cident_check", "k_rlc_ident_lines", "k_lines_fold<3>",
                "k_rlc_ident_check", "k_lines_sig_list", "k_verify_list"],
     "aggregate": ["k_lagrange", "k_aggregate", "k_aggregate_finish"],
 }

@@ -42,6 +42,11 @@ __global__ void TBG_LAUNCH k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A
 //                    the Fp2 coordinates split over the pair (bls_pair.h).
 __global__ void TBG_LAUNCH_N(TBG_DECODE_WAVES) k_decode_sigs(DevBatch B) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // The chain's first kernel zeroes its work-list counters and level 0's
+  // bucket sizes (a runtime memset kernel queued behind other streams' waves
+  // held each chain for ~2 ms in the pipelined bench)
+  if (i < CNT_WORDS) B.counters[i] = 0;
+  if (B.rlc_batch && i <= MSM_BUCKETS) B.msm_off[i] = 0;
   if (i >= B.n_partials) return;
   uint8_t b[96];
   for (int j = 0; j < 96; ++j) b[j] = B.sigs[96ull * i + j];
@@ -79,9 +84,11 @@ void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x
   if (n) TBG_KLAUNCH(k_decode_pubkeys, grid_for(n), dim3(kBlock), st, pk48, n, out, out_x, status);
 }
 void launch_decode_sigs(const DevBatch& B, hipStream_t st) {
-  if (!B.n_partials) return;
-  TBG_KLAUNCH(k_decode_sigs, grid_for(B.n_partials), dim3(kBlock), st, B);
-  TBG_KLAUNCH(k_subgroup_sigs, grid_for(2 * B.n_partials), dim3(kBlock), st, B);
+  // at least enough lanes to zero the counters (and level 0's bucket sizes)
+  uint32_t lanes = B.n_partials > CNT_WORDS ? B.n_partials : CNT_WORDS;
+  if (B.rlc_batch && lanes < MSM_BUCKETS + 1) lanes = MSM_BUCKETS + 1;
+  TBG_KLAUNCH(k_decode_sigs, grid_for(lanes), dim3(kBlock), st, B);
+  if (B.n_partials) TBG_KLAUNCH(k_subgroup_sigs, grid_for(2 * B.n_partials), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

@@ -15,7 +15,8 @@
 //   k_rlc_g1_l0      one lane per partial: r_i, [r_i] pk_i, bucket sizes
 //   k_msm_scan       bucket offsets (one workgroup)
 //   k_msm_scatter    bucket entries
-//   k_msm_bucket     one lane PAIR per bucket: its sum times (2j + 1)
+//   k_msm_bucket_part  one lane PAIR per quarter of a bucket: its sum
+//   k_msm_bucket     one lane PAIR per bucket: the quarters' sum times (2j + 1)
 //   k_msm_sum        tree sums (fan-in 16), the last one in affine form
 #define TBG_ADD_DBL_INLINE 1
 #ifndef TBG_SCHED_FENCE
@@ -115,18 +116,34 @@ __device__ __forceinline__ Aff<Fp2x> px_psi_k(const G2A& s, uint32_t k, bool neg
   return p;
 }
 
-// One lane pair per bucket j: the sum of its entries, times (2j + 1).
+// Bucket sums in two kernels so that no lane pair runs a long chain: a pair
+// per (bucket j, slice of its entries) adds its slice (~20 mixed additions),
+// then a pair per bucket adds the MSM_SPLIT slice sums and multiplies by
+// (2j + 1) (one pair per bucket running all ~80 additions and the scaling
+// took 5.0 ms per 160k-DV launch, latency-bound on 1,024 waves).
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket_part(DevBatch B) {
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
+  if (w >= MSM_BUCKETS * MSM_SPLIT) return;
+  if (B.counters[CNT_L0_BAD]) return;
+  const uint32_t j = w / MSM_SPLIT, sl = w % MSM_SPLIT;
+  const uint32_t o0 = B.msm_off[j], n = B.msm_off[j + 1] - o0;
+  const uint32_t e0 = o0 + (n * sl) / MSM_SPLIT, e1 = o0 + (n * (sl + 1)) / MSM_SPLIT;
+  Jac<Fp2x> acc = jac_inf<Fp2x>();
+#pragma unroll 1
+  for (uint32_t e = e0; e < e1; ++e) {
+    const uint32_t v = B.msm_ent[e];
+    acc = jac_add_aff_in(acc, px_psi_k(B.sig_aff[v >> 3], (v >> 1) & 3u, (v & 1u) != 0));
+  }
+  px_store(B.msm_part[w], acc);
+}
+
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
-  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
+  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (j >= MSM_BUCKETS) return;
   if (B.counters[CNT_L0_BAD]) return;
-  Jac<Fp2x> acc = jac_inf<Fp2x>();
-  const uint32_t e1 = B.msm_off[j + 1];
+  Jac<Fp2x> acc = px_load(B.msm_part[MSM_SPLIT * j]);
 #pragma unroll 1
-  for (uint32_t e = B.msm_off[j]; e < e1; ++e) {
-    const uint32_t w = B.msm_ent[e];
-    acc = jac_add_aff_in(acc, px_psi_k(B.sig_aff[w >> 3], (w >> 1) & 3u, (w & 1u) != 0));
-  }
+  for (uint32_t sl = 1; sl < MSM_SPLIT; ++sl) acc = jac_add_in<Fp2x, true>(acc, px_load(B.msm_part[MSM_SPLIT * j + sl]));
   const uint32_t m = 2 * j + 1;
   if (m > 1 && !jac_is_inf(acc)) {
     const Jac<Fp2x> b = acc;
@@ -171,10 +188,11 @@ void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, 
 
 // Level 0 up to S's lines: G1 products and P_d (k_rlc_duty_sum), then the MSM.
 void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
-  hipMemsetAsync(B.msm_off, 0, 4ull * (MSM_BUCKETS + 1), st);
+  // (msm_off was zeroed by k_decode_sigs, the chain's first kernel)
   if (B.n_partials) TBG_KLAUNCH(k_rlc_g1_l0, grid_for(B.n_partials), dim3(kBlock), st, B, pk_tab, pk_status, n_pk);
   TBG_KLAUNCH(k_msm_scan, dim3(1), dim3(kScanBlock), st, B);
   if (B.n_partials) TBG_KLAUNCH(k_msm_scatter, grid_for(B.n_partials), dim3(kBlock), st, B);
+  TBG_KLAUNCH(k_msm_bucket_part, grid_for(2 * MSM_BUCKETS * MSM_SPLIT), dim3(kBlock), st, B);
   TBG_KLAUNCH(k_msm_bucket, grid_for(2 * MSM_BUCKETS), dim3(kBlock), st, B);
   const G2J* in = B.msm_bkt;
   uint32_t n = MSM_BUCKETS;

@@ -304,20 +304,43 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   hipStream_t st = sl.st, st2 = sl.st2;
   const bool verify = B.op != TBG_OP_AGGREGATE;
   const G1A* pk = (const G1A*)c->d_pk;
+  // With one stream per slot the two independent chains run one after the
+  // other, the per-message chain first.  TBG_ALT_ORDER=1 runs the
+  // per-signature chain first on odd slots (to stagger the latency-bound
+  // phases of batches submitted together): measured no better.
+  static const int alt_order = [] {
+    // A/B knob (measured: no gain at 20 or 48 steps, slightly worse at 48):
+    // 1 = odd slots run the per-signature chain first
+    const char* e = getenv("TBG_ALT_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  const bool sig_first = alt_order && st2 == st && ((&sl - c->slots.data()) & 1);
+  auto msg_chain = [&]() -> int {
+    HIP_TRY(hipEventRecord(ev[3], st2));
+    if (verify) launch_hash_msgs(B, st2);
+    HIP_TRY(hipEventRecord(ev[4], st2));
+    if (verify) launch_h_lines(B, st2);
+    HIP_TRY(hipEventRecord(ev[5], st2));
+    return TBG_OK;
+  };
+  auto sig_chain = [&]() -> int {
+    HIP_TRY(hipEventRecord(ev[10], st));
+    launch_decode_sigs(B, st);  // zeroes B.counters (and level 0's bucket sizes) first
+    HIP_TRY(hipEventRecord(ev[1], st));
+    if (verify)
+      launch_rlc_prepare(B, pk, (const G1A*)c->d_xpk, (const G1A*)c->d_pktab, (const int32_t*)c->d_pk_status, c->n_pk,
+                         st);
+    HIP_TRY(hipEventRecord(ev[2], st));
+    return TBG_OK;
+  };
   HIP_TRY(hipEventRecord(ev[0], st));
   HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
-  HIP_TRY(hipEventRecord(ev[3], st2));
-  if (verify) launch_hash_msgs(B, st2);
-  HIP_TRY(hipEventRecord(ev[4], st2));
-  if (verify) launch_h_lines(B, st2);
-  HIP_TRY(hipEventRecord(ev[5], st2));
-  HIP_TRY(hipEventRecord(ev[10], st));
-  HIP_TRY(hipMemsetAsync(B.counters, 0, 4 * CNT_WORDS, st));
-  launch_decode_sigs(B, st);
-  HIP_TRY(hipEventRecord(ev[1], st));
-  if (verify)
-    launch_rlc_prepare(B, pk, (const G1A*)c->d_xpk, (const G1A*)c->d_pktab, (const int32_t*)c->d_pk_status, c->n_pk, st);
-  HIP_TRY(hipEventRecord(ev[2], st));
+  int rc;
+  if (sig_first) {
+    if ((rc = sig_chain()) != TBG_OK || (rc = msg_chain()) != TBG_OK) return rc;
+  } else {
+    if ((rc = msg_chain()) != TBG_OK || (rc = sig_chain()) != TBG_OK) return rc;
+  }
   HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
   HIP_TRY(hipEventRecord(ev[6], st));
   if (verify) launch_rlc_check(B, pk, (const G1A*)c->d_xpk, (const int32_t*)c->d_pk_status, c->n_pk, st);
@@ -469,6 +492,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_mcur = sec(l0 ? 4ull * MSM_BUCKETS : 0);
   size_t w_ment = sec(l0 ? 16ull * np : 0);
   size_t w_mbkt = sec(l0 ? sizeof(G2J) * (size_t)MSM_BUCKETS : 0);
+  size_t w_mpart = sec(l0 ? sizeof(G2J) * (size_t)MSM_BUCKETS * MSM_SPLIT : 0);
   size_t w_msum = sec(l0 ? sizeof(G2J) * (size_t)MSM_SUM_ENTRIES : 0);
   size_t w_bpt = sec(l0 ? sizeof(G2A) : 0);
   size_t w_blines = sec(l0 ? 4ull * LINES_WORDS : 0);
@@ -608,6 +632,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.msm_cur = (uint32_t*)(dw + w_mcur);
   B.msm_ent = (uint32_t*)(dw + w_ment);
   B.msm_bkt = (G2J*)(dw + w_mbkt);
+  B.msm_part = (G2J*)(dw + w_mpart);
   B.msm_sum = (G2J*)(dw + w_msum);
   B.batch_pt = (G2A*)(dw + w_bpt);
   B.batch_lines = (uint32_t*)(dw + w_blines);

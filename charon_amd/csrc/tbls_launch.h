@@ -91,6 +91,7 @@ struct DevBatch {
   uint32_t* msm_off;      // [MSM_BUCKETS + 1] bucket sizes, then their offsets
   uint32_t* msm_cur;      // [MSM_BUCKETS] scatter cursors
   uint32_t* msm_ent;      // [4 n_partials] bucket entries: partial << 3 | k << 1 | negative
+  G2J* msm_part;          // [MSM_BUCKETS * MSM_SPLIT] sums of the bucket slices
   G2J* msm_bkt;           // [MSM_BUCKETS] (2j + 1) * (bucket j's sum)
   G2J* msm_sum;           // [MSM_SUM_ENTRIES] tree sums of msm_bkt
   G2A* batch_pt;          // [1] S in affine form
@@ -118,6 +119,7 @@ enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS =
 // (|a| - 1) / 2; the tree sums fold MSM_SUM_FAN points per thread.
 constexpr uint32_t MSM_BUCKETS = 32768;
 constexpr uint32_t MSM_SUM_FAN = 16;
+constexpr uint32_t MSM_SPLIT = 4;  // slices per bucket (k_msm_bucket_part)
 constexpr uint32_t MSM_SUM_ENTRIES = MSM_BUCKETS / MSM_SUM_FAN + MSM_BUCKETS / (MSM_SUM_FAN * MSM_SUM_FAN) + 16;
 // Level-0 product tree over the groups' P-chunk products (fan-in 16 per quad).
 constexpr uint32_t L0_TREE_FAN = 16;

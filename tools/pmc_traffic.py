@@ -12,17 +12,45 @@ import os
 import sys
 
 
+# kernels that only load keys / generate test vectors (not part of the chain)
+NOT_CHAIN = {"k_sign", "k_sk_to_pk", "k_decode_pubkeys", "k_pubkey_tables"}
+# chain kernels that vector generation also launches (on one batch at a time):
+# only their largest-grid calls belong to the chain
+SHARED = {"k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"}
+
+
+def _grid(r):
+    for k in ("Grid_Size", "Grid_Size_X", "Grid_Sizes"):
+        if k in r:
+            try:
+                return int(str(r[k]).split(",")[0].strip("[( "))
+            except ValueError:
+                pass
+    return 0
+
+
 def main(src, dst, batches=1):
+    """KB per CHAIN launch for every kernel: the sum over the kernel's calls in
+    the chain launches (several per launch for k_msm_sum, k_l0_tree, the two
+    k_rlc_miller_chunks modes, ...) / the number of chain launches (the calls
+    of k_decode_sigs, which runs once per chain and nowhere else)."""
     out = {}
     for sub, c in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
         agg = collections.defaultdict(list)
         with open(os.path.join(src, sub, "run_counter_collection.csv")) as f:
             for r in csv.DictReader(f):
                 if r["Counter_Name"] == c:
-                    agg[r["Kernel_Name"].split("(")[0].replace("tbg::", "")].append(float(r["Counter_Value"]))
+                    name = r["Kernel_Name"].split("(")[0].replace("tbg::", "").replace("void ", "")
+                    agg[name].append((_grid(r), float(r["Counter_Value"])))
+        chains = max(1, len(agg.get("k_decode_sigs", [])))
         for k, v in agg.items():
-            out.setdefault(k, {})[c + "_KB_per_launch"] = round(sum(v) / len(v), 1)
-            out[k]["launches"] = len(v)
+            if k in NOT_CHAIN:
+                continue
+            if k in SHARED:
+                g = max(x for x, _ in v)
+                v = [x for x in v if x[0] == g]
+            out.setdefault(k, {})[c + "_KB_per_launch"] = round(sum(y for _, y in v) / chains, 1)
+            out[k]["calls_per_launch"] = round(len(v) / chains, 2)
     doc = {"command": "rocprofv3 --pmc FETCH_SIZE (resp. WRITE_SIZE) -f csv -- python3 bench.py --no-cpu "
                       "--inflight 1 --merge %d --steps %d --warmup 0 --api-batches 0 (tools/gpu_pmc.sh)" % (batches, batches),
            "note": "one counter group per pass; raw values in KB per launch.  bench.py counts FETCH_SIZE x 2 (the "
