@@ -93,7 +93,8 @@ TBG_HD void sha256_dst_prime(Sha256& s) {
   sha256_byte(s, (uint8_t)DST_LEN);
 }
 
-// expand_message_xmd(msg, DST, 256): out[256]
+// expand_message_xmd(msg, DST, 256): out[256]  (byte-stream reference form;
+// the kernels use expand_message_xmd_256w below)
 TBG_NI void expand_message_xmd_256(const uint8_t* msg, uint32_t msg_len, uint8_t* out) {
   Sha256 s;
   sha256_init(s);
@@ -120,6 +121,119 @@ TBG_NI void expand_message_xmd_256(const uint8_t* msg, uint32_t msg_len, uint8_t
   }
 }
 
+// ---- word-oriented form: every block is 16 big-endian words built in
+// registers and compressed with a fully unrolled, 16-word rolling schedule
+// (the byte-stream form above keeps its buffers and the 64-word schedule in
+// scratch memory: ~14 KB of scratch traffic per message).
+TBG_HD constexpr uint32_t dstp_byte(int i) {  // DST_prime = DST || I2OSP(len(DST), 1)
+  return i < DST_LEN ? (uint32_t)(uint8_t)"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"[i] : (uint32_t)DST_LEN;
+}
+TBG_HD constexpr uint32_t dstp_word(int i) {  // big-endian word of DST_prime bytes [i, i + 4)
+  return (dstp_byte(i) << 24) | (dstp_byte(i + 1) << 16) | (dstp_byte(i + 2) << 8) | dstp_byte(i + 3);
+}
+
+TBG_HD void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[16]) {
+  constexpr uint32_t K[64] = {
+      0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+      0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+      0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+      0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+      0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+      0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+      0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+      0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    if (i >= 16) {
+      const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      w[i & 15] += s0 + w[(i - 7) & 15] + s1;
+    }
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = hh + S1 + ch + K[i] + w[i & 15];
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+TBG_HD void sha256_iv(uint32_t (&h)[8]) {
+  h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
+  h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
+}
+
+// Byte p of b_0's input after Z_pad: msg || I2OSP(256, 2) || I2OSP(0, 1) ||
+// DST_prime || 0x80 || 0...; the last 8 bytes of block nb - 1 carry the bit
+// length (with Z_pad) and are filled in by the caller.
+TBG_HD uint32_t b0_stream_byte(const uint8_t* msg, uint32_t L, uint32_t p) {
+  if (p < L) return msg[p];
+  if (p == L) return 0x01;
+  if (p < L + 3) return 0x00;
+  if (p < L + 3 + DST_LEN + 1) return dstp_byte((int)(p - L - 3));
+  return p == L + 3 + DST_LEN + 1 ? 0x80u : 0u;
+}
+
+// out[64]: the 256 output bytes as big-endian words.
+TBG_HD void expand_message_xmd_256w(const uint8_t* msg, uint32_t L, uint32_t (&out)[64]) {
+  uint32_t h[8], w[16];
+  sha256_iv(h);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = 0;
+  sha256_compress(h, w);  // Z_pad: one block of zeros
+  const uint32_t tail = L + 3 + DST_LEN + 1;  // bytes after Z_pad, before the padding
+  const uint32_t nb = (tail + 1 + 8 + 63) / 64;
+  const uint64_t bits = 8ull * (64 + tail);
+#pragma unroll 1
+  for (uint32_t blk = 0; blk < nb; ++blk) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t p = 64 * blk + 4 * k;
+      w[k] = (b0_stream_byte(msg, L, p) << 24) | (b0_stream_byte(msg, L, p + 1) << 16) |
+             (b0_stream_byte(msg, L, p + 2) << 8) | b0_stream_byte(msg, L, p + 3);
+    }
+    if (blk == nb - 1) {
+      w[14] = (uint32_t)(bits >> 32);
+      w[15] = (uint32_t)bits;
+    }
+    sha256_compress(h, w);
+  }
+  uint32_t b0[8], bi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    b0[k] = h[k];
+    bi[k] = 0;  // b_1 = H(b_0 || 1 || DST_prime) = H(strxor(b_0, 0) || ...)
+  }
+#pragma unroll 1
+  for (uint32_t i = 1; i <= 8; ++i) {
+    // block 1: strxor(b_0, b_(i-1)) || I2OSP(i, 1) || DST_prime[0 .. 31)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = b0[k] ^ bi[k];
+    w[8] = (i << 24) | (dstp_byte(0) << 16) | (dstp_byte(1) << 8) | dstp_byte(2);
+#pragma unroll
+    for (int k = 9; k < 16; ++k) w[k] = dstp_word(3 + 4 * (k - 9));
+    sha256_iv(h);
+    sha256_compress(h, w);
+    // block 2: DST_prime[31 .. 44) || 0x80 || 0... || bit length 77 * 8
+    w[0] = dstp_word(31);
+    w[1] = dstp_word(35);
+    w[2] = dstp_word(39);
+    w[3] = (dstp_byte(43) << 24) | 0x800000u;
+#pragma unroll
+    for (int k = 4; k < 15; ++k) w[k] = 0;
+    w[15] = 77 * 8;
+    sha256_compress(h, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bi[k] = h[k];
+      out[8 * (i - 1) + k] = h[k];
+    }
+  }
+}
+
 // 32 big-endian bytes -> 14 limbs (value < 2^256)
 TBG_HD Fp limbs_from_be32(const uint8_t* b) {
   Fp r = fp_zero();
@@ -140,7 +254,39 @@ TBG_HD Fp fp_from_be64_mod(const uint8_t* b) {
   return fp_mul2(hi, ca, lo, cb);
 }
 
+// 8 big-endian words (a 256-bit value) -> 14 limbs
+TBG_HD Fp limbs_from_be_words8(const uint32_t* w) {
+  Fp r = fp_zero();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int bit = 32 * (7 - j);  // position of word j's lowest bit
+    const uint32_t v = w[j];
+    const int li = bit / 28, off = bit % 28;
+    r.l[li] |= (v << off) & LMASK;
+    if (li + 1 < NL) r.l[li + 1] |= (v >> (28 - off)) & LMASK;
+    if (off > 24 && li + 2 < NL) r.l[li + 2] |= v >> (56 - off);
+  }
+  return r;
+}
+
+// 16 big-endian words mod p, in Montgomery form (as fp_from_be64_mod)
+TBG_HD Fp fp_from_be_words16_mod(const uint32_t* w) {
+  Fp hi = limbs_from_be_words8(w), lo = limbs_from_be_words8(w + 8);
+  Fp ca = fp_from_const(R2_2E256_M), cb = fp_from_const(R2_M);
+  return fp_mul2(hi, ca, lo, cb);
+}
+
 TBG_HD void hash_to_field_fp2(const uint8_t* msg, uint32_t msg_len, Fp2& u0, Fp2& u1) {
+  uint32_t uni[64];
+  expand_message_xmd_256w(msg, msg_len, uni);
+  u0.c0 = fp_from_be_words16_mod(uni);
+  u0.c1 = fp_from_be_words16_mod(uni + 16);
+  u1.c0 = fp_from_be_words16_mod(uni + 32);
+  u1.c1 = fp_from_be_words16_mod(uni + 48);
+}
+
+// the byte-stream reference form (host tests compare the two)
+TBG_HD void hash_to_field_fp2_bytes(const uint8_t* msg, uint32_t msg_len, Fp2& u0, Fp2& u1) {
   uint8_t uni[256];
   expand_message_xmd_256(msg, msg_len, uni);
   u0.c0 = fp_from_be64_mod(uni);

@@ -617,3 +617,12 @@ void hc_stage_g2_add(void) {
   a = jac_add_in<Fp2, true>(a, b);
 }
 }  // extern "C"
+
+// expand_message_xmd / hash_to_field: the word-oriented register form the
+// kernels use against the byte-stream reference form.
+extern "C" int hc_h2f_check(const uint8_t* msg, uint32_t len) {
+  Fp2 a0, a1, b0, b1;
+  hash_to_field_fp2(msg, len, a0, a1);
+  hash_to_field_fp2_bytes(msg, len, b0, b1);
+  return fp2_eq(a0, b0) && fp2_eq(a1, b1) ? 1 : 0;
+}

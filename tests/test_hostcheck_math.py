@@ -385,3 +385,16 @@ def test_level0_bucket_msm_matches_rlc_products():
         buf = b"".join(ss)
         arr = (ctypes.c_uint64 * len(rr))(*rr)
         assert L.hc_msm_check(buf, arr, len(ss)) == 1
+
+
+def test_word_sha_expand_message_matches_byte_stream():
+    """The kernels' expand_message_xmd (16-word blocks in registers, unrolled
+    SHA-256 schedule) equals the byte-stream form on every message length
+    around the block boundaries (b_0's input is 64 + len + 47 bytes)."""
+    import ctypes
+    L = lib()
+    L.hc_h2f_check.restype = ctypes.c_int
+    L.hc_h2f_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+    for n in list(range(0, 20)) + [31, 32, 33, 63, 64, 65, 71, 72, 73, 127, 128, 136, 200, 255, 300]:
+        msg = bytes((7 * k + n) & 0xFF for k in range(n))
+        assert L.hc_h2f_check(msg, n) == 1, n
