@@ -25,54 +25,36 @@ __device__ __forceinline__ Jac<Fp2x> px_psi(const Jac<Fp2x>& p) {
   return {f_mulc(f_conj(p.X), PSI_X), f_mulc(f_conj(p.Y), PSI_Y), f_reduce(f_conj(p.Z))};
 }
 
-// The two [x] loops use the additions without the P == Q branch (bls_pair.h
-// jac_add_x: fewer live registers); an addition that meets it -- only for
-// points of tiny order -- flags the message, which is then cleared on the
-// single-lane reference path (g2_clear_cofactor, out of line) and skipped by
-// the later kernels.  h_status (written by k_hash_affine afterwards) holds
-// the flag.
-constexpr int32_t CLEAR_DONE = 2;
-
-__device__ __noinline__ void clear_reference(const DevBatch& B, uint32_t m) {
-  const G2J h = g2_clear_cofactor(B.h_jac[m]);
-  if (pair_par() == 0) {
-    B.h_jac[m] = h;
-    B.h_status[m] = CLEAR_DONE;
+// [x] p = -[|x|] p (63 doublings, 5 additions; the P == Q case doubles inline)
+__device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
+  Jac<Fp2x> acc = p;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    acc = jac_dbl_in(acc);
+    if ((X_ABS >> i) & 1) acc = jac_add_in<Fp2x, true>(acc, p);
   }
+  return jac_neg(acc);
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x1(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (m >= B.n_msgs) return;
   const Jac<Fp2x> p = px_load(B.h_jac[m]);
-  bool exc = false;
-  const Jac<Fp2x> t1 = jac_neg(jac_mul_xabs_x(p, exc));  // [x]P
-  const Jac<Fp2x> u = jac_add_x(t1, px_psi(p), exc);
-  if (exc) {
-    clear_reference(B, m);
-    return;
-  }
-  if (pair_par() == 0) B.h_status[m] = 0;
+  const Jac<Fp2x> t1 = px_mul_x(p);
   px_store(B.h_jac[B.n_msgs + m], t1);
-  px_store(B.h_jac[2 * B.n_msgs + m], u);
+  px_store(B.h_jac[2 * B.n_msgs + m], jac_add_in<Fp2x, true>(t1, px_psi(p)));
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x2(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
-  if (m >= B.n_msgs || B.h_status[m] == CLEAR_DONE) return;
+  if (m >= B.n_msgs) return;
   G2J* u = B.h_jac + 2 * B.n_msgs + m;
-  bool exc = false;
-  const Jac<Fp2x> v = jac_neg(jac_mul_xabs_x(px_load(*u), exc));
-  if (exc) {
-    clear_reference(B, m);
-    return;
-  }
-  px_store(*u, v);
+  px_store(*u, px_mul_x(px_load(*u)));
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_fin(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
-  if (m >= B.n_msgs || B.h_status[m] == CLEAR_DONE) return;
+  if (m >= B.n_msgs) return;
   const Jac<Fp2x> p = px_load(B.h_jac[m]);
   const Jac<Fp2x> psi_p = px_psi(p);
   Jac<Fp2x> t3 = px_psi(px_psi(jac_dbl_in(p)));                       // psi^2(2P)
