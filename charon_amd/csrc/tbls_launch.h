@@ -121,9 +121,13 @@ constexpr uint32_t MSM_BUCKETS = 32768;
 constexpr uint32_t MSM_SUM_FAN = 16;
 constexpr uint32_t MSM_SPLIT = 4;  // slices per bucket (k_msm_bucket_part)
 constexpr uint32_t MSM_SUM_ENTRIES = MSM_BUCKETS / MSM_SUM_FAN + MSM_BUCKETS / (MSM_SUM_FAN * MSM_SUM_FAN) + 16;
-// Level-0 product tree over the groups' P-chunk products (fan-in 16 per quad).
-constexpr uint32_t L0_TREE_FAN = 16;
-TBG_HD inline uint32_t grp_f_entries(uint32_t n_groups) { return n_groups + n_groups / (L0_TREE_FAN - 1) + 2 * L0_TREE_FAN; }
+// Level-0 product tree over the groups' P-chunk products.  Each pass is a
+// chain of F - 1 Fp12 products on one lane group (~24 us each at one wave per
+// SIMD), so the tree's latency ~ log_F(n) * F is smallest near F = 4 (16: 1.3
+// ms for 10k groups; 4: ~0.7 ms) -- it sits on every launch's critical path.
+constexpr uint32_t L0_TREE_FAN = 4;
+// (sum over the passes of ceil(n / F^k) <= n / (F - 1) + one per pass)
+TBG_HD inline uint32_t grp_f_entries(uint32_t n_groups) { return n_groups + n_groups / (L0_TREE_FAN - 1) + 40; }
 // k_rlc_miller_chunks modes
 enum MillerMode : int { MILLER_GROUPS = 0, MILLER_L0 = 1, MILLER_GROUP_S = 2 };
 // k_rlc_duty_sum phases
