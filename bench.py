@@ -320,7 +320,11 @@ def main():
     # rehearsal of N ranks can share one card (identity on an 8-GPU node)
     import torch
     device = local % max(1, torch.cuda.device_count())
-    e = eng.Engine(device, slots=max(args.inflight, 1), verify_mode=args.verify_mode, rlc_group=args.rlc_group,
+    # one slot more than the replayed launches: the product-path side key packs
+    # the next group into it while `inflight` launches run (the replay uses
+    # only the first `inflight` slots)
+    e = eng.Engine(device, slots=max(args.inflight, 1) + (1 if args.api_batches else 0),
+                   verify_mode=args.verify_mode, rlc_group=args.rlc_group,
                    rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot)
     # `inflight` engine slots each hold `merge` independent 10k-DV batches
     # submitted together (tbg_submit_group: one device batch, one launch per
@@ -400,7 +404,7 @@ def main():
     roofline, roofline_isolated, roofline_pipeline = stage_rooflines(work_model(), iso, kernel_ms, args, value / ws,
                                                                      args.steps, l0=l0_state == eng.L0_PASSED)
     # (reuses the engine's slots: after the replays and the isolated pass)
-    api = api_pipeline(e, eng, flat, args.inflight, args.api_batches, M) if args.api_batches else None
+    api = api_pipeline(e, eng, flat, args.inflight + 1, args.api_batches, M) if args.api_batches else None
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "DV-duties/s (n verifies + 1 aggregate each)",

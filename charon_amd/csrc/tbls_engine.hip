@@ -12,6 +12,7 @@
 #include <mutex>
 #include <new>
 #include <random>
+#include <thread>
 #include <vector>
 #include "tbls_launch.h"
 #include "bls_lines.h"
@@ -520,18 +521,36 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   uint32_t* duty_first = (uint32_t*)(h + o_duty_first);
   uint32_t* thr = (uint32_t*)(h + o_thr);
   uint32_t* pd = (uint32_t*)(h + o_pduty);
-  uint32_t D = 0, P = 0, M = 0, MB = 0;
+  // offsets first, then every caller batch packed by its own worker (the
+  // sections are disjoint): a 16-batch group is ~70 MB of host copies, which
+  // one thread would take longer to pack than the GPU takes to run it
   std::vector<Part> parts(n_batches);
+  std::vector<uint32_t> mb0(n_batches);
+  uint32_t D = 0, P = 0, M = 0, MB = 0;
   for (uint32_t k = 0; k < n_batches; ++k) {
     const tbg_batch* b = bs[k];
-    const uint32_t bnd = b->n_duties, bnp = b->n_partials, bnm = verify ? b->n_msgs : 0;
+    parts[k].d0 = D;
+    parts[k].nd = b->n_duties;
+    parts[k].p0 = P;
+    parts[k].np = b->n_partials;
+    parts[k].m0 = M;
+    parts[k].nm = verify ? b->n_msgs : 0;
+    mb0[k] = MB;
+    D += parts[k].nd;
+    P += parts[k].np;
+    M += parts[k].nm;
+    if (verify) MB += b->msg_off[b->n_msgs];
+  }
+  auto pack = [&](uint32_t k) {
+    const tbg_batch* b = bs[k];
+    const uint32_t D = parts[k].d0, P = parts[k].p0, M = parts[k].m0, MB = mb0[k];
+    const uint32_t bnd = b->n_duties, bnp = b->n_partials, bnm = parts[k].nm;
     if (verify) {
       const uint32_t bmb = b->msg_off[bnm];
       if (bmb) memcpy(h + o_msgs + MB, b->msgs, bmb);
       for (uint32_t m = 0; m < bnm; ++m) msg_off[M + m] = MB + b->msg_off[m];
       for (uint32_t d = 0; d < bnd; ++d) duty_msg[D + d] = M + b->duty_msg[d];
       memcpy(h + o_pk + 4ull * P, b->pubkey_ids, 4ull * bnp);
-      MB += bmb;
     }
     for (uint32_t d = 0; d < bnd; ++d) {
       duty_first[D + d] = P + b->duty_first[d];
@@ -543,15 +562,17 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
       memcpy(h + o_sigs + 96ull * P, b->sigs, 96ull * bnp);
       memcpy(h + o_ids + P, b->identifiers, bnp);
     }
-    parts[k].d0 = D;
-    parts[k].nd = bnd;
-    parts[k].p0 = P;
-    parts[k].np = bnp;
-    parts[k].m0 = M;
-    parts[k].nm = bnm;
-    D += bnd;
-    P += bnp;
-    M += bnm;
+  };
+  const uint32_t workers = (np >= (1u << 16) && n_batches > 1) ? std::min<uint32_t>(n_batches, 8) : 1;
+  if (workers == 1) {
+    for (uint32_t k = 0; k < n_batches; ++k) pack(k);
+  } else {
+    std::vector<std::thread> th;
+    for (uint32_t w = 0; w < workers; ++w)
+      th.emplace_back([&, w] {
+        for (uint32_t k = w; k < n_batches; k += workers) pack(k);
+      });
+    for (auto& t : th) t.join();
   }
   duty_first[nd] = np;
   if (verify) msg_off[nm] = MB;
