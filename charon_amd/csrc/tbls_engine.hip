@@ -69,6 +69,7 @@ struct Slot {
   hipEvent_t ev[kChainEvents] = {};  // see launch_chain
   hipEvent_t done = nullptr;
   float ms[8] = {};
+  uint64_t seen_bad = 0, seen_total = 0;  // invalid / verified partials of the parts collected so far
   tbg::DevBatch B{};           // device view of the last batch (resident until the slot is reused)
   size_t w_out = 0;
 };
@@ -84,7 +85,8 @@ struct tbg_ctx {
   G1A* d_pktab = nullptr;  // [2 per entry] pk + [x]pk, pk - [x]pk (level 0's G1 products, k_msm.hip)
   int32_t* d_pk_status = nullptr;
   uint32_t n_pk = 0, cap_pk = 0;
-  std::vector<void*> retired;  // outgrown pubkey tables (see tbg_load_pubkeys)
+  hipEvent_t retire_ev = nullptr;  // orders frees of outgrown pubkey tables after the slots' queued work
+  hipEvent_t keys_ready = nullptr;  // the key table's last load / growth (slot streams wait on it)
   std::vector<Slot> slots;
   tbg_ticket next_ticket = 1;
   float last_ms[8] = {};
@@ -170,7 +172,11 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   if (cfg && cfg->rlc_batch > TBG_RLC_L0_OFF) { delete c; return TBG_E_INVALID_ARG; }
   if (cfg) c->rlc_batch = cfg->rlc_batch;
   c->rlc_seed = cfg ? cfg->rlc_seed : 0;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->retire_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->keys_ready, hipEventDisableTiming) != hipSuccess) {
+    if (c->retire_ev) hipEventDestroy(c->retire_ev);
+    if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return TBG_E_DEVICE;
   }
@@ -178,8 +184,11 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // overlap on the GPU (one batch's latency-bound stages fill the CUs the
   // other leaves idle).
   uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 3;
-  if (nslots > TBG_MAX_SLOTS || (cfg && cfg->streams_per_slot > 2)) {
+  const uint32_t spp = (cfg && cfg->streams_per_slot > 1) ? cfg->streams_per_slot : 1;
+  if (nslots > TBG_MAX_SLOTS || spp > 2 || nslots * spp > TBG_MAX_SLOT_STREAMS) {
     hipStreamDestroy(c->stream);
+    hipEventDestroy(c->retire_ev);
+    hipEventDestroy(c->keys_ready);
     delete c;
     return TBG_E_INVALID_ARG;
   }
@@ -221,12 +230,15 @@ void tbg_destroy(tbg_ctx* c) {
     if (s.st2 && s.st2 != s.st) hipStreamDestroy(s.st2);
     if (s.st) hipStreamDestroy(s.st);
   }
-  if (c->d_pk) hipFree(c->d_pk);
-  if (c->d_xpk) hipFree(c->d_xpk);
-  if (c->d_pktab) hipFree(c->d_pktab);
-  if (c->d_pk_status) hipFree(c->d_pk_status);
-  for (void* p : c->retired) hipFree(p);
-  if (c->stream) hipStreamDestroy(c->stream);
+  // the key tables are stream-ordered allocations of the utility stream
+  if (c->stream) {
+    for (void* p : {(void*)c->d_pk, (void*)c->d_xpk, (void*)c->d_pktab, (void*)c->d_pk_status})
+      if (p) hipFreeAsync(p, c->stream);
+    hipStreamSynchronize(c->stream);
+    hipStreamDestroy(c->stream);
+  }
+  if (c->retire_ev) hipEventDestroy(c->retire_ev);
+  if (c->keys_ready) hipEventDestroy(c->keys_ready);
   delete c;
 }
 
@@ -238,36 +250,42 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   HIP_TRY(hipSetDevice(c->device));
   if (c->n_pk + (uint64_t)count > 0xFFFFFFF0ull) return TBG_E_INVALID_ARG;
   uint32_t need = c->n_pk + count;
+  void* old_tabs[4] = {nullptr, nullptr, nullptr, nullptr};  // outgrown tables, freed below
   if (need > c->cap_pk) {
+    // Stream-ordered allocations on the utility stream: no device-wide
+    // synchronisation (hipMalloc / hipFree would wait for every batch in flight).
     uint32_t ncap = need + need / 2 + 1024;
     G1A* npk = nullptr;
     G1A* nxpk = nullptr;
     G1A* ntab = nullptr;
     int32_t* nst = nullptr;
-    if (hipMalloc(&npk, sizeof(G1A) * (size_t)ncap) != hipSuccess) return TBG_E_OOM;
-    if (hipMalloc(&nxpk, sizeof(G1A) * (size_t)ncap) != hipSuccess) { hipFree(npk); return TBG_E_OOM; }
-    if (hipMalloc(&ntab, 2 * sizeof(G1A) * (size_t)ncap) != hipSuccess) { hipFree(npk); hipFree(nxpk); return TBG_E_OOM; }
-    if (hipMalloc(&nst, sizeof(int32_t) * (size_t)ncap) != hipSuccess) {
-      hipFree(npk);
-      hipFree(nxpk);
-      hipFree(ntab);
+    hipStream_t us = c->stream;
+    if (hipMallocAsync((void**)&npk, sizeof(G1A) * (size_t)ncap, us) != hipSuccess) return TBG_E_OOM;
+    if (hipMallocAsync((void**)&nxpk, sizeof(G1A) * (size_t)ncap, us) != hipSuccess) {
+      hipFreeAsync(npk, us);
+      return TBG_E_OOM;
+    }
+    if (hipMallocAsync((void**)&ntab, 2 * sizeof(G1A) * (size_t)ncap, us) != hipSuccess) {
+      hipFreeAsync(npk, us);
+      hipFreeAsync(nxpk, us);
+      return TBG_E_OOM;
+    }
+    if (hipMallocAsync((void**)&nst, sizeof(int32_t) * (size_t)ncap, us) != hipSuccess) {
+      hipFreeAsync(npk, us);
+      hipFreeAsync(nxpk, us);
+      hipFreeAsync(ntab, us);
       return TBG_E_OOM;
     }
     if (c->n_pk) {
-      HIP_TRY(hipMemcpyAsync(npk, c->d_pk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
-      HIP_TRY(hipMemcpyAsync(nxpk, c->d_xpk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
-      HIP_TRY(hipMemcpyAsync(ntab, c->d_pktab, 2 * sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
-      HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(npk, c->d_pk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
+      HIP_TRY(hipMemcpyAsync(nxpk, c->d_xpk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
+      HIP_TRY(hipMemcpyAsync(ntab, c->d_pktab, 2 * sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
+      HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    // Batches already in flight captured the old table's address in their
-    // kernel arguments: retire it (freed by tbg_destroy) instead of waiting
-    // for every slot.  Growth is geometric, so retired tables stay below 2x
-    // the final one.
-    if (c->d_pk) c->retired.push_back(c->d_pk);
-    if (c->d_xpk) c->retired.push_back(c->d_xpk);
-    if (c->d_pktab) c->retired.push_back(c->d_pktab);
-    if (c->d_pk_status) c->retired.push_back(c->d_pk_status);
+    old_tabs[0] = c->d_pk;
+    old_tabs[1] = c->d_xpk;
+    old_tabs[2] = c->d_pktab;
+    old_tabs[3] = c->d_pk_status;
     c->d_pk = npk;
     c->d_xpk = nxpk;
     c->d_pktab = ntab;
@@ -275,10 +293,10 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
     c->cap_pk = ncap;
   }
   if (first_id) *first_id = c->n_pk;
-  if (count == 0) return TBG_OK;
-  uint8_t* d_bytes = nullptr;
-  if (hipMalloc(&d_bytes, 48ull * count) != hipSuccess) return TBG_E_OOM;
+  uint8_t* d_bytes = nullptr;  // stream-ordered staging (freed on the same stream)
+  if (count && hipMallocAsync((void**)&d_bytes, 48ull * count, c->stream) != hipSuccess) return TBG_E_OOM;
   int rc = TBG_OK;
+  if (count == 0) goto ready;
   if (hipMemcpyAsync(d_bytes, pk48, 48ull * count, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
   if (rc == TBG_OK) {
     launch_decode_pubkeys(d_bytes, count, c->d_pk + c->n_pk, c->d_xpk + c->n_pk, c->d_pk_status + c->n_pk, c->stream);
@@ -289,8 +307,24 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   if (rc == TBG_OK && status &&
       hipMemcpyAsync(status, c->d_pk_status + c->n_pk, sizeof(int32_t) * count, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
     rc = TBG_E_DEVICE;
-  if (hipStreamSynchronize(c->stream) != hipSuccess) rc = TBG_E_DEVICE;
-  hipFree(d_bytes);
+ready:
+  // Submits order their slot streams after this event, not after the frees below.
+  if (hipEventRecord(c->keys_ready, c->stream) != hipSuccess) rc = TBG_E_DEVICE;
+  if (old_tabs[0]) {
+    // Batches already queued on the slot streams captured the old tables'
+    // addresses: their free is ordered after everything queued so far on
+    // every slot stream (one event recorded per stream, waited on by the
+    // utility stream), without blocking the host or the device.
+    for (auto& sl : c->slots)
+      for (hipStream_t q : {sl.st, sl.st2}) {
+        if (!q || (q == sl.st2 && sl.st2 == sl.st)) continue;
+        if (hipEventRecord(c->retire_ev, q) != hipSuccess || hipStreamWaitEvent(c->stream, c->retire_ev, 0) != hipSuccess)
+          rc = TBG_E_DEVICE;
+      }
+    for (void* p : old_tabs) hipFreeAsync(p, c->stream);
+  }
+  if (d_bytes) hipFreeAsync(d_bytes, c->stream);
+  if (hipEventSynchronize(c->keys_ready) != hipSuccess) rc = TBG_E_DEVICE;
   if (rc == TBG_OK) c->n_pk += count;
   return rc;
 }
@@ -663,8 +697,9 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.agg_list = (uint32_t*)(dw + w_alist);
 
   hipStream_t st = s->st;
-  // The resident pubkey table may have been (re)loaded on the utility stream.
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  // The resident pubkey table may have been (re)loaded on the utility stream
+  // (already complete: tbg_load_pubkeys waits for it; ordered anyway).
+  HIP_TRY(hipStreamWaitEvent(st, c->keys_ready, 0));
   HIP_TRY(hipMemcpyAsync(s->d_in, s->h_in, in_bytes, hipMemcpyHostToDevice, st));
   rc = launch_chain(c, *s, B, s->ev);
   if (rc != TBG_OK) return rc;
@@ -677,6 +712,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
     tickets[k] = parts[k].ticket;
   }
   s->parts = std::move(parts);
+  s->seen_bad = s->seen_total = 0;
   s->busy = true;
   s->ticket = s->parts[0].ticket;
   s->op = op;
@@ -749,11 +785,18 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     const int32_t* st = (const int32_t*)s->h_out;  // partial statuses lead the output region
     uint32_t bad = 0;
     for (uint32_t i = 0; i < q->np; ++i) bad += st[q->p0 + i] == TBG_PS_INVALID ? 1u : 0u;
-    c->invalid_ema = 0.5 * c->invalid_ema + 0.5 * (double)bad / q->np;
+    s->seen_bad += bad;
+    s->seen_total += q->np;
   }
   chain_times(s->ev, s->ms);
   memcpy(c->last_ms, s->ms, sizeof(c->last_ms));
   part_done(s, q);
+  // One update per DEVICE batch, over all of its parts (whatever order they
+  // are collected in), once its last part is collected.
+  if (!s->busy && s->seen_total) {
+    c->invalid_ema = 0.5 * c->invalid_ema + 0.5 * (double)s->seen_bad / (double)s->seen_total;
+    s->seen_bad = s->seen_total = 0;
+  }
   return TBG_OK;
 }
 

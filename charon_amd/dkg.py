@@ -9,7 +9,8 @@
                            (plain sums: the multi-signature of all shares)
   verify_multi_signature   dkg/dkg.go:377       VerifyMultiSignature
   lock_verify_signatures   cluster/lock.go:137-179  the lock's aggregate
-                           signature: FastAggregateVerify over every pubshare
+                           signature: FastAggregateVerify over every pubshare,
+                           over the hash the caller recomputed (not the JSON's)
 
 Each step is one GPU submit over the whole ceremony (every DV and peer at
 once) instead of the reference's per-partial loop: the deposit data runs as a
@@ -21,8 +22,9 @@ through tbg_sum_pubkeys, tbg_sum_sigs and tbg_fast_aggregate_verify.
 Errors mirror the reference's strings; where the reference iterates a Go map
 (random order) the first error in the caller's order is raised.  Out of scope
 (host work off the signature path): the definition's operator ECDSA
-signatures (Definition.VerifySignatures) and hashLock's SSZ walk -- the lock
-hash is taken as given.
+signatures (Definition.VerifySignatures) and hashLock's SSZ walk -- the
+caller passes the lock hash it recomputed; the JSON's lock_hash is only
+compared against it.
 """
 from __future__ import annotations
 
@@ -165,10 +167,21 @@ def _lock_bytes(v) -> bytes:
     return base64.b64decode(v)
 
 
-def lock_verify_signatures(lock: dict, engine=None) -> None:
-    """Lock.VerifySignatures' aggregate check (cluster/lock.go:142-177) over a
+def lock_verify_signatures(lock: dict, lock_hash: bytes | None = None, engine=None) -> None:
+    """Lock.VerifySignatures' aggregate check (cluster/lock.go:137-177) over a
     lock in its JSON form: cluster_definition.version, signature_aggregate,
-    lock_hash, distributed_validators[].public_shares."""
+    distributed_validators[].public_shares.
+
+    The reference verifies the aggregate over hashLock(l), the hash it
+    recomputes from the lock's fields (lock.go:166), never over the lock_hash
+    the JSON carries.  hashLock's SSZ walk of the definition and validators is
+    host work outside this path, so the CALLER supplies the hash it recomputed
+    as `lock_hash`; without it this raises (ValueError) instead of trusting
+    the file.  A JSON lock_hash that differs from the recomputed one fails as
+    VerifyHashes does (lock.go:117-131, "invalid lock hash").  The
+    definition's operator signatures (Definition.VerifySignatures,
+    lock.go:138-140) are ECDSA work outside the BLS path and are not checked
+    here."""
     version = lock.get("cluster_definition", {}).get("version", "")
     sig = _lock_bytes(lock.get("signature_aggregate"))
     if not sig:
@@ -177,6 +190,15 @@ def lock_verify_signatures(lock: dict, engine=None) -> None:
         raise DKGError("empty lock aggregate signature")
     if len(sig) != 96:  # (the reference's (*[96]byte) conversion would panic)
         raise DKGError("uncompress sig: invalid length")
+    if lock_hash is None:
+        raise ValueError("lock_verify_signatures needs the caller's recomputed hashLock(l) (cluster/lock.go:166); "
+                         "the lock_hash field of the JSON is not trusted")
+    lock_hash = bytes(lock_hash)
+    if len(lock_hash) != 32:
+        raise ValueError("lock_hash must be the 32-byte hashLock(l)")
+    claimed = _lock_bytes(lock.get("lock_hash"))
+    if claimed and claimed != lock_hash:
+        raise DKGError("invalid lock hash")
     e = tbls._engine(engine)
     _, st, sst = e.sum_sigs(sig, [0, 1])  # tblsconv.SigFromBytes: decode only
     if _is_decode_error(int(sst[0])):
@@ -187,7 +209,6 @@ def lock_verify_signatures(lock: dict, engine=None) -> None:
         if isinstance(k, Exception):
             raise DKGError(str(k))
     ids = tbls._pk_cache.ids_for(e, raws)
-    h = _lock_bytes(lock.get("lock_hash"))
-    out = e.fast_aggregate_verify(ids, [0, len(ids)], [h], sig)
+    out = e.fast_aggregate_verify(ids, [0, len(ids)], [lock_hash], sig)
     if int(out[0]) != eng.PS_VALID:
         raise DKGError("invalid lock signature aggregate")

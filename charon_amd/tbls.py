@@ -99,19 +99,33 @@ _DUTY_ERRORS = {
 
 class _PubkeyCache:
     """Resident pubkey ids per engine (the startup pubshare upload of
-    app/app.go:334-376 happens here, lazily)."""
+    app/app.go:334-376 happens here, lazily).  Every distinct key is uploaded
+    (decoded into the device table) once per engine; its table id and decode
+    status are kept, so repeated lookups never grow the device table."""
 
     def __init__(self):
         self.ids = {}
+        self.status = {}
 
-    def ids_for(self, e: eng.Engine, keys):
+    def _load(self, e: eng.Engine, keys):
+        """Upload the keys not resident yet; returns (id cache, status cache)."""
         cache = self.ids.setdefault(e.uid, {})
+        stat = self.status.setdefault(e.uid, {})
         missing = [k for k in dict.fromkeys(keys) if k not in cache]
         if missing:
-            first, _ = e.load_pubkeys(b"".join(missing))
-            for i, k in enumerate(missing):
+            first, st = e.load_pubkeys(b"".join(missing))
+            for i, (k, s) in enumerate(zip(missing, st.tolist())):
                 cache[k] = first + i
+                stat[k] = int(s)
+        return cache, stat
+
+    def ids_for(self, e: eng.Engine, keys):
+        cache, _ = self._load(e, keys)
         return [cache[k] for k in keys]
+
+    def statuses_for(self, e: eng.Engine, keys):
+        _, stat = self._load(e, keys)
+        return [stat[k] for k in keys]
 
 
 _pk_cache = _PubkeyCache()
@@ -137,12 +151,9 @@ def key_from_bytes_batch(raws, engine=None):
     for r in raws:
         if len(r) != 48:
             raise TblsError("unmarshal pubkey: invalid length")
-    first, st = e.load_pubkeys(b"".join(raws))
-    cache = _pk_cache.ids.setdefault(e.uid, {})
     out = []
-    for i, (r, s) in enumerate(zip(raws, st.tolist())):
+    for r, s in zip(raws, _pk_cache.statuses_for(e, raws)):  # only keys not resident yet are uploaded
         if s == 0:
-            cache.setdefault(r, first + i)
             out.append(PublicKey(r))
         else:
             out.append(TblsError("unmarshal pubkey: " + _PK_ERRORS.get(s, str(s))))

@@ -70,11 +70,15 @@ typedef enum {
 typedef struct tbg_ctx tbg_ctx;
 typedef uint64_t tbg_ticket;
 
-/* Upper bound of tbg_config.slots: every slot owns one or two HIP streams,
- * and past ~16 streams per process the HSA runtime runs out of queue
- * resources (observed on MI355X), so larger values are refused with
- * TBG_E_INVALID_ARG instead of failing inside HIP. */
+/* Bounds of tbg_config.slots and of the streams they own: every slot owns
+ * streams_per_slot (1 or 2) HIP streams, and past ~16 streams per process the
+ * HSA runtime runs out of queue resources (observed on MI355X).  tbg_init
+ * refuses slots > TBG_MAX_SLOTS and slots * streams_per_slot >
+ * TBG_MAX_SLOT_STREAMS with TBG_E_INVALID_ARG instead of failing inside HIP.
+ * The bound is per context: several contexts on ONE device (tbg_multi_init
+ * with a repeated ordinal) add their streams up, so keep their sum below it. */
 #define TBG_MAX_SLOTS 12
+#define TBG_MAX_SLOT_STREAMS 16
 
 typedef struct {
   int32_t device;         /* HIP device ordinal                           */
@@ -101,7 +105,8 @@ typedef struct {
 #define TBG_VERIFY_RLC 0
 #define TBG_VERIFY_EACH 1
 /* Adaptive level-1 group size (rlc_group = 0): an exponential average (weight
- * 1/2 per collected batch) of the invalid share of verified partials picks
+ * 1/2 per device batch, i.e. per tbg_submit_group, updated once every part of
+ * it is collected) of the invalid share of verified partials picks
  * the group for the next submit (measured at 1 % invalid: 8 beats 16 by 1 %,
  * at 0 % 16 beats 8 by 6 %). */
 #define TBG_RLC_AUTO_TO8 0.003

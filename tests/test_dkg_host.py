@@ -23,6 +23,18 @@ def test_empty_aggregate_rules_need_no_gpu():
             dkg.lock_verify_signatures({"cluster_definition": {"version": v}, "signature_aggregate": None})
 
 
+def test_lock_verify_needs_a_recomputed_hash():
+    """The reference checks the aggregate over hashLock(l) (cluster/lock.go:166),
+    not the JSON's lock_hash: without the caller's hash nothing is trusted."""
+    from charon_amd import dkg
+    lock = {"cluster_definition": {"version": "v1.4.0"}, "lock_hash": "0x" + bytes(32).hex(),
+            "signature_aggregate": "0x" + (b"\x80" + bytes(95)).hex()}
+    with pytest.raises(ValueError, match="recomputed hashLock"):
+        dkg.lock_verify_signatures(lock)
+    with pytest.raises(dkg.DKGError, match="^invalid lock hash$"):
+        dkg.lock_verify_signatures(lock, b"\x01" * 32)
+
+
 def test_lock_byte_fields_decode_both_encodings():
     from charon_amd import dkg
     versions = [l["cluster_definition"]["version"] for l in LOCKS]
@@ -34,7 +46,7 @@ def test_lock_byte_fields_decode_both_encodings():
         # rejected before any key or pairing work
         assert len(dkg._lock_bytes(l["signature_aggregate"])) == 32
         with pytest.raises(dkg.DKGError, match="uncompress sig: invalid length"):
-            dkg.lock_verify_signatures(l)
+            dkg.lock_verify_signatures(l, bytes(32))
 
 
 def test_fixture_deposit_aggregates_are_the_golden_signatures():

@@ -109,20 +109,47 @@ def test_lock_verify_signatures(engine):
             "signature_aggregate": "0x" + G["lock"]["aggregate_signature"],
             "distributed_validators": [{"public_shares": ["0x" + shares[pk][p.share_idx].hex() for p in data[pk]]}
                                        for pk in data]}
-    dkg.lock_verify_signatures(lock, engine)
-    tampered = dict(lock, lock_hash="0x" + bytes(32).hex())
+    dkg.lock_verify_signatures(lock, h, engine)
+    # the aggregate is checked over the caller's recomputed hash, never the JSON's
+    with pytest.raises(ValueError, match="recomputed hashLock"):
+        dkg.lock_verify_signatures(lock, None, engine)
+    edited = dict(lock, lock_hash="0x" + bytes(32).hex())  # JSON hash no longer the recomputed one
+    with pytest.raises(dkg.DKGError, match="^invalid lock hash$"):
+        dkg.lock_verify_signatures(edited, h, engine)
+    wrong = bytes(32)  # a lock whose fields hash differently: same JSON hash and aggregate
+    with pytest.raises(dkg.DKGError, match="^invalid lock hash$"):
+        dkg.lock_verify_signatures(lock, wrong, engine)
+    unclaimed = {k: v for k, v in lock.items() if k != "lock_hash"}
     with pytest.raises(dkg.DKGError, match="^invalid lock signature aggregate$"):
-        dkg.lock_verify_signatures(tampered, engine)
+        dkg.lock_verify_signatures(unclaimed, wrong, engine)
     missing = dict(lock, distributed_validators=lock["distributed_validators"][:-1])
     with pytest.raises(dkg.DKGError, match="^invalid lock signature aggregate$"):
-        dkg.lock_verify_signatures(missing, engine)
+        dkg.lock_verify_signatures(missing, h, engine)
     badkey = json.loads(json.dumps(lock))
     badkey["distributed_validators"][0]["public_shares"][0] = "0x" + (b"\x00" * 48).hex()
     with pytest.raises(dkg.DKGError, match="^unmarshal pubkey: "):
-        dkg.lock_verify_signatures(badkey, engine)
+        dkg.lock_verify_signatures(badkey, h, engine)
     badsig = dict(lock, signature_aggregate="0x" + (b"\x00" * 96).hex())
     with pytest.raises(dkg.DKGError, match="^uncompress sig: "):
-        dkg.lock_verify_signatures(badsig, engine)
+        dkg.lock_verify_signatures(badsig, h, engine)
+
+
+def test_key_upload_is_deduplicated(engine):
+    """KeyFromBytes over keys already resident uploads nothing more (the
+    device table does not grow with repeated lock / wiring checks), and a bad
+    key keeps reporting its decode error from the cached status."""
+    from charon_amd import tbls
+    _, shares, _ = _deposit_inputs()
+    raws = [k for per in shares.values() for k in per.values()]
+    tbls.key_from_bytes_batch(raws, engine)
+    n0 = engine.pubkey_count
+    bad = b"\x00" * 48
+    r1 = tbls.key_from_bytes_batch(raws + [bad] + raws, engine)
+    assert engine.pubkey_count == n0 + 1
+    r2 = tbls.key_from_bytes_batch([bad] + raws, engine)
+    assert engine.pubkey_count == n0 + 1
+    assert isinstance(r1[len(raws)], tbls.TblsError) and str(r1[len(raws)]) == str(r2[0])
+    assert all(isinstance(k, tbls.PublicKey) for k in r2[1:])
 
 
 def test_sum_edge_cases(engine):
