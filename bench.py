@@ -116,41 +116,92 @@ def work_model():
 STAGE_KERNELS = {
     "decode": ["k_decode_sigs", "k_subgroup_sigs"],
     "hash": ["k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
-    "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_sum", "k_msm_scan", "k_msm_scatter", "k_rlc_duty_sum",
-                "k_lines_fold<4>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<0>"],
+    "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_bucket_part", "k_msm_sum", "k_msm_scan", "k_msm_scatter",
+                "k_rlc_duty_sum", "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines",
+                "k_lines_fold<FOLD_GROUPS>"],
     "h_lines": ["k_lines_h"],
-    "verify": ["k_rlc_miller_chunks", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after", "k_rlc_group_final",
-               "k_rlc_resolve_groups", "k_rlc_chunk_lines", "k_lines_fold<1>", "k_rlc_check_chunks",
-               "k_rlc_cident_lines", "k_lines_fold<2>", "k_rlc_cident_check", "k_rlc_ident_lines", "k_lines_fold<3>",
-               "k_rlc_ident_check", "k_lines_sig_list", "k_verify_list"],
+    "verify": ["k_rlc_miller_chunks<MILLER_L0>", "k_rlc_miller_chunks<MILLER_GROUP_S>",
+               "k_rlc_miller_chunks<MILLER_GROUPS>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after",
+               "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_chunk_lines", "k_lines_fold<FOLD_CHUNKS>",
+               "k_rlc_check_chunks", "k_rlc_cident_lines", "k_lines_fold<FOLD_CID>", "k_rlc_cident_check",
+               "k_rlc_ident_lines", "k_lines_fold<FOLD_IDENT>", "k_rlc_ident_check", "k_lines_sig_list",
+               "k_verify_list"],
     "aggregate": ["k_lagrange", "k_aggregate", "k_aggregate_finish"],
+}
+# profile name (launch site) -> the symbol rocprofv3 prints for it
+ROCPROF_NAME = {
+    "k_rlc_miller_chunks<MILLER_L0>": "void tbg::k_rlc_miller_chunks<1>(tbg::DevBatch)",
+    "k_rlc_miller_chunks<MILLER_GROUP_S>": "void tbg::k_rlc_miller_chunks<2>(tbg::DevBatch)",
+    "k_rlc_miller_chunks<MILLER_GROUPS>": "void tbg::k_rlc_miller_chunks<0>(tbg::DevBatch)",
 }
 
 
-def stage_mads(wm, args, l0=False):
-    """Algorithmic u32 mul-adds per launch of each stage for one clean launch
-    of `merge` batches (work model of tools/count_work.py: RLC group G = 16,
-    chunk C = 4).  l0: the level-0 schedule (k_msm.hip) -- per partial the G1
-    table product and 4 bucket additions, per launch the bucket scalings, tree
-    sums, S's lines, S's Miller quad and one final exponentiation."""
-    m = wm["mads"]
-    nd, n = args.dvs * max(1, getattr(args, "merge", 1)), args.n  # one launch covers `merge` batches
-    np_ = nd * n
-    G = wm.get("rlc_schedule", {}).get("group", 16)
-    ng = (nd + G - 1) // G
-    out = {
-        "decode": m["decode_sig"] * np_,
-        "hash": m["hash_to_g2"] * nd,
-        "combine": m["rlc_partial"] * (np_ - ng) + m["rlc_duty_sum_4"] * nd + m["rlc_group_lines"] * ng,
-        "h_lines": m["lines_h"] * nd,
-        "verify": m["rlc_check_per_group"] * ng,
-        "aggregate": m["aggregate_3of4_all4"] * nd,
-    }
-    if l0:
-        out["combine"] = (m["l0_partial"] * np_ + m["l0_duty_sum_4"] * nd + m["l0_bucket_scales"]
-                          + (32768 + 2048 + 128 + 8) * m["g2_add"] + m["lines_h"])
-        out["verify"] = m["l0_per_group"] * ng + m["l0_s_quad"] + m["final_exp_quad"]
+def kernel_profile(prof):
+    """[(kernel, ms)] of one device batch replayed alone -> {kernel: (ms, launches)}."""
+    out = {}
+    for name, ms in prof:
+        t, n = out.get(name, (0.0, 0))
+        out[name] = (t + ms, n + 1)
     return out
+
+
+def launch_items(groups, G):
+    """Items of one device batch (the `merge` caller batches of a slot)."""
+    nd = sum(b.n_dv for b in groups)
+    np_ = sum(len(b.identifiers) for b in groups)
+    nm = sum(len(b.msg_off) - 1 for b in groups)
+    ng = -(-nd // G)  # level-1 groups are cut from the packed device batch
+    return {"partial": np_, "message": nm, "duty": nd, "group": ng, "launch": 1}
+
+
+def kernel_roofline(wm, kp, items, tm, batches):
+    """roofline: the dominant kernel of one device batch replayed ALONE (every
+    kernel timed by its own HIP event pair on its stream, tbg_replay_profile)
+    -- its algorithmic u32 mul-adds (per-kernel work model of
+    tools/count_work.py x the launch's items) / its measured duration."""
+    if not wm or "kernels" not in wm:
+        return None
+    model = wm["kernels"]
+    dom = max(kp, key=lambda k: kp[k][0])
+    priced = [k for k in sorted(kp, key=lambda k: -kp[k][0]) if k in model]
+    if not priced:
+        return None
+    k = dom if dom in model else priced[0]
+    m = model[k]
+    mads = m["mads"] * items[m["per"]] + m.get("plus_per_launch", 0)
+    ms, launches = kp[k]
+    ach = mads / (ms * 1e-3) / 1e12
+    short = k.split("<")[0]
+    traffic = None
+    if tm and short in tm.get("kernels", {}):
+        kk = tm["kernels"][short]
+        traffic = int(1024 * (2 * kk.get("FETCH_SIZE_KB_per_launch", 0) + kk.get("WRITE_SIZE_KB_per_launch", 0))
+                      * batches / max(1, tm.get("batches_per_launch", 1)))
+    return {"bound": "valu-int-mul", "kernel": k, "rocprof_name": ROCPROF_NAME.get(k, "tbg::" + k + "(...)"),
+            "achieved": round(ach, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
+            "frac": round(ach / PEAK_MAD_TOPS, 4), "traffic": traffic,
+            "algorithmic_mads_per_launch": int(mads), "work_model": f"{m['mads']} mads per {m['per']}"
+            + (f" + {m['plus_per_launch']} per launch" if m.get("plus_per_launch") else ""),
+            "items_per_launch": items[m["per"]], "launch_ms": round(ms / launches, 4),
+            "batches_per_launch": batches, "dominant_by_exclusive_time": dom,
+            "measured": "HIP event pair around every kernel of ONE device batch replayed alone on its stream "
+                        "(tbg_replay_profile, after the timed region); rocprofv3 --kernel-trace of the same "
+                        "command: tools/roofline_from_trace.py"}
+
+
+def pipeline_roofline(wm, value, l0, t, n):
+    """roofline_pipeline: the whole chain, work model x rate (config 2 shape)."""
+    if not wm or (t, n) != (3, 4):
+        return None
+    unit = wm["mads"]["unit_3of4_l0" if l0 else "unit_3of4_rlc"]
+    ach = value * unit / 1e12
+    return {"bound": "valu-int-mul", "kernel": "the whole kernel chain (launches in flight together)",
+            "achieved": round(ach, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
+            "frac": round(ach / PEAK_MAD_TOPS, 4), "work_per_unit_mads": unit,
+            "schedule": "level 0 (batch-wide check, bucket MSM)" if l0 else "level-1 groups",
+            "reference_schedule_mads_per_unit": wm["mads"]["unit_3of4_single_lane_schedule"],
+            "reference_schedule_equivalent_tmads": round(value * wm["mads"]["unit_3of4_single_lane_schedule"] / 1e12,
+                                                         3)}
 
 
 def traffic_model():
@@ -161,64 +212,6 @@ def traffic_model():
         with open(path) as f:
             return json.load(f)
     return None
-
-
-def stage_traffic(tm, stage, batches):
-    """HBM bytes per launch of `batches` batches for a stage's kernels, from
-    the committed PMC passes (FETCH_SIZE x 2, the gfx950 correction of
-    MI355X_MICROARCH.md, + WRITE_SIZE), scaled from the PMC run's launch size."""
-    if not tm:
-        return None
-    kk = tm.get("kernels", {})
-    names = [k for k in STAGE_KERNELS[stage] if k in kk]
-    if not names:
-        return None
-    per_batch = sum(1024 * (2 * kk[k].get("FETCH_SIZE_KB_per_launch", 0) + kk[k].get("WRITE_SIZE_KB_per_launch", 0))
-                    for k in names) / max(1, tm.get("batches_per_launch", 1))
-    return int(per_batch * batches)
-
-
-def stage_rooflines(wm, iso, timed, args, value, steps, l0=False):
-    """roofline: the dominant stage of the timed region -- its algorithmic
-    mul-adds over the timed steps / the summed HIP-event durations of its
-    launches (on the slot streams they ran on); with launches in flight
-    together those durations include sharing the CUs, so this is a lower
-    bound.  roofline_isolated: the same stage, one launch alone.
-    roofline_pipeline: the whole chain, work / wall time."""
-    if not wm or args.t != 3 or args.n != 4:
-        return None, None, None
-    M = max(1, getattr(args, "merge", 1))
-    per_launch = stage_mads(wm, args, l0)
-    per_batch = {k: v / M for k, v in per_launch.items()}
-    tm = traffic_model()
-    stage = max(per_batch, key=lambda k: timed.get(k, 0.0))
-    total_ms = timed[stage]
-    ach = per_batch[stage] * steps / (total_ms * 1e-3) / 1e12
-    n_launch = -(-steps // M)
-    roofline = {"bound": "valu-int-mul", "kernel": f"{stage} stage: " + " + ".join(STAGE_KERNELS[stage][:3]),
-                "achieved": round(ach, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
-                "frac": round(ach / PEAK_MAD_TOPS, 4), "traffic": stage_traffic(tm, stage, M),
-                "algorithmic_mads_per_launch": int(per_batch[stage] * M), "launches": n_launch,
-                "avg_launch_ms": round(total_ms / max(1, steps / M), 3),
-                "measured": "HIP events around the stage on its slot's stream, timed region"}
-    iso_stage = max(per_batch, key=lambda k: iso.get(k, 0.0))
-    ach_i = per_batch[iso_stage] * M / (iso[iso_stage] * 1e-3) / 1e12
-    isolated = {"bound": "valu-int-mul", "kernel": f"{iso_stage} stage: " + " + ".join(STAGE_KERNELS[iso_stage][:3]),
-                "achieved": round(ach_i, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
-                "frac": round(ach_i / PEAK_MAD_TOPS, 4), "traffic": stage_traffic(tm, iso_stage, M),
-                "algorithmic_mads_per_launch": int(per_batch[iso_stage] * M), "launch_ms": round(iso[iso_stage], 3),
-                "batches_per_launch": M}
-    unit = round(sum(per_launch.values()) / (args.dvs * M))  # mul-adds per DV-duty of this schedule
-    ach_p = value * unit / 1e12
-    pipeline = {"bound": "valu-int-mul", "kernel": "the whole kernel chain (launches in flight together)",
-                "achieved": round(ach_p, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
-                "frac": round(ach_p / PEAK_MAD_TOPS, 4),
-                "traffic": (sum(stage_traffic(tm, s_, 1) or 0 for s_ in STAGE_KERNELS) or None) if tm else None,
-                "work_per_unit_mads": unit, "schedule": "level 0 (batch-wide check, bucket MSM)" if l0 else
-                "level-1 groups",
-                "reference_schedule_mads_per_unit": wm["mads"]["unit_3of4_single_lane_schedule"],
-                "reference_schedule_equivalent_tmads": round(value * wm["mads"]["unit_3of4_single_lane_schedule"] / 1e12, 3)}
-    return roofline, isolated, pipeline
 
 
 def cpu_baseline(batch, seconds: float):
@@ -288,6 +281,15 @@ def batch_exact(res, b, eng):
     return bool(np.array_equal(res.agg[ok], b.group_sig[ok]))
 
 
+WORKLOADS = {
+    "config2": "config2: 3-of-4, {dvs} DVs x 1 attestation per GPU",
+    "config3": "config3: 7-of-10, {dvs} DVs x 1 attestation per GPU",
+    "config4": "config4: 3-of-4, {dvs}-DV shard per GPU of the 1M-DV batch",
+    "config5": "config5: {dvs} mixed DV-duties per GPU (attestation / sync / randao / proposal, thresholds 3-of-4, "
+               "5-of-7, 7-of-10), {inject:.0%} invalid partials of every kind",
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -301,20 +303,22 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--inflight", type=int, default=3, help="engine slots replayed round-robin (launches in flight)")
     ap.add_argument("--merge", type=int, default=16,
-                    help="10k-DV batches per slot, submitted together as one device batch (tbg_submit_group)")
+                    help="caller batches per slot, submitted together as one device batch (tbg_submit_group)")
     ap.add_argument("--launches", type=int, default=0,
                     help="spread the timed steps over at least this many launches (default: one per slot)")
     ap.add_argument("--verify-mode", type=int, default=0, help="0 = RLC groups with fallback, 1 = per-partial checks")
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
-    ap.add_argument("--inject", type=float, default=0.0,
-                    help="fraction of partials replaced by invalid ones (side measurement; the headline is 0)")
+    ap.add_argument("--inject", type=float, default=None,
+                    help="fraction of partials replaced by invalid ones (side measurement; the headline is 0; "
+                         "config5 defaults to 0.01)")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (read at HIP init); default: the environment's / HIP's 4")
-    ap.add_argument("--workload", choices=["config2", "config4"], default="config2",
-                    help="config2: 10k 3-of-4 DVs per step (the headline); config4: each GPU's 125k-DV shard of "
-                         "the 1M-DV 3-of-4 batch of BASELINE config 4")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2",
+                    help="config2: 10k 3-of-4 DVs per step (the headline); config3: 100k 7-of-10 DVs per step; "
+                         "config4: each GPU's 125k-DV shard of the 1M-DV 3-of-4 batch; config5: 10k mixed duties "
+                         "with 1%% invalid partials of every kind per step")
     ap.add_argument("--api-batches", type=int, default=192,
                     help="batches pushed through the product path (tbg_submit / tbg_collect, host packing and PCIe "
                          "included) for the api_pipeline side key; 0 skips it")
@@ -322,10 +326,17 @@ def main():
     if args.workload == "config4":
         args.dvs, args.t, args.n = 125000, 3, 4
         args.inflight, args.merge = min(args.inflight, 2), 1  # ~19 GB of HBM per resident 125k-DV batch
+    elif args.workload == "config3":
+        args.dvs, args.t, args.n = 100000, 7, 10
+        args.inflight, args.merge = min(args.inflight, 3), 1  # one 100k-DV batch (1M partials) per launch
+    if args.inject is None:
+        args.inject = 0.01 if args.workload == "config5" else 0.0
+    if args.workload != "config2":
+        args.api_batches = 0  # the product-path side key is measured on the headline shape
 
     ws, rank, local = dist_setup()
     from charon_amd import engine as eng
-    from tools.workload import make_batch
+    from tools.workload import make_batch, make_mixed_batch
 
     # one GPU per rank (LOCAL_RANK); modulo the visible count so a gloo
     # rehearsal of N ranks can share one card (identity on an 8-GPU node)
@@ -337,29 +348,33 @@ def main():
     e = eng.Engine(device, slots=max(args.inflight, 1) + (1 if args.api_batches else 0),
                    verify_mode=args.verify_mode, rlc_group=args.rlc_group,
                    rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot)
-    # `inflight` engine slots each hold `merge` independent 10k-DV batches
+    # `inflight` engine slots each hold `merge` independent caller batches
     # submitted together (tbg_submit_group: one device batch, one launch per
     # kernel for all of them) and stay resident; the timed region replays the
     # slots round-robin, so `merge` steps run per launch and `inflight`
     # launches overlap -- what back-to-back submits of a serving node do.
     M = max(1, args.merge)
+
+    def mk(seed, inject):
+        if args.workload == "config5":
+            return make_mixed_batch(e, args.dvs, seed=seed, inject=inject)
+        return make_batch(e, args.dvs, args.t, args.n, seed=seed, inject=inject)
+
+    def as_call(b):
+        return dict(duty_first=b.duty_first, sigs=b.sigs, identifiers=b.identifiers, msgs=(b.msg_data, b.msg_off),
+                    duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+
     batches, tickets = [], []
     pcie_ms = None
     if args.rlc_group == 0 and args.verify_mode == 0 and args.inject > 0:
         # the adaptive group size (tbg_config.rlc_group = 0) follows the invalid
         # share of collected batches: one untimed pass puts it in the state a
         # node serving this traffic is in before the resident slots are built
-        cal = [make_batch(e, args.dvs, args.t, args.n, seed=args.seed + 999_983, inject=args.inject) for _ in range(2)]
-        for b in cal:
-            e.collect(e.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers,
-                               msgs=(b.msg_data, b.msg_off), duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids,
-                               duty_threshold=b.threshold))
+        for b in [mk(args.seed + 999_983 + k, args.inject) for k in range(2)]:
+            e.collect(e.submit(eng.OP_VERIFY_AGGREGATE, **as_call(b)))
     for j in range(args.inflight):
-        group = [make_batch(e, args.dvs, args.t, args.n, seed=args.seed + 1000 * rank + M * j + k, inject=args.inject)
-                 for k in range(M)]
-        ts = e.submit_group(eng.OP_VERIFY_AGGREGATE, [
-            dict(duty_first=b.duty_first, sigs=b.sigs, identifiers=b.identifiers, msgs=(b.msg_data, b.msg_off),
-                 duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold) for b in group])
+        group = [mk(args.seed + 1000 * rank + M * j + k, args.inject) for k in range(M)]
+        ts = e.submit_group(eng.OP_VERIFY_AGGREGATE, [as_call(b) for b in group])
         for b, t in zip(group, ts):
             first = e.collect(t)
             if pcie_ms is None:
@@ -396,7 +411,7 @@ def main():
     # outputs of the timed replays must still be exact (every batch of every slot)
     for group, t0 in zip(batches, tickets):
         for k, b in enumerate(group):
-            again = e.fetch(t0 + k, b.n_dv, b.n_dv * b.n)
+            again = e.fetch(t0 + k, b.n_dv, len(b.identifiers))
             assert batch_exact(again, b, eng)
     b = batches[0][0]
     flat = [x for g in batches for x in g]
@@ -407,13 +422,17 @@ def main():
     value = units / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # Isolated pass (untimed): one resident slot (`merge` batches) alone on the
-    # GPU, per-stage HIP events on its stream -- the per-launch durations the
-    # roofline uses (pipelined, every stage shares the CUs with the others).
-    iso = e.replay(tickets[0], 1)
+    # Per-kernel pass (untimed): one resident device batch (`merge` batches)
+    # replayed alone, an event pair around every kernel -- the exclusive
+    # durations the roofline prices; the stage sums are isolated_batch_ms.
+    kp = kernel_profile(e.replay_profile(tickets[0]))
+    iso = {st: round(sum(kp[k][0] for k in ks if k in kp), 3) for st, ks in STAGE_KERNELS.items()}
+    iso["total"] = round(sum(v[0] for v in kp.values()), 3)
+    wm = work_model()
+    roofline = kernel_roofline(wm, kp, launch_items(batches[0], group_used or 16), traffic_model(), M)
     # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
-    roofline, roofline_isolated, roofline_pipeline = stage_rooflines(work_model(), iso, kernel_ms, args, value / ws,
-                                                                     args.steps, l0=l0_state == eng.L0_PASSED)
+    roofline_pipeline = pipeline_roofline(wm, value / ws, l0_state == eng.L0_PASSED, args.t, args.n) \
+        if args.workload in ("config2", "config4") else None
     # (reuses the engine's slots: after the replays and the isolated pass)
     api = api_pipeline(e, eng, flat, args.inflight + 1, args.api_batches, M) if args.api_batches else None
 
@@ -423,10 +442,8 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 14x28-bit limbs)",
         "data": "synthetic (seeded shares/pubshares/signatures generated on the GPU)"
                 + (f", {args.inject:.2%} injected invalid partials" if args.inject else ""),
-        "config": {"workload": (f"config2: {args.t}-of-{args.n}, {args.dvs} DVs x 1 attestation per GPU"
-                                if args.workload == "config2" else
-                                f"config4: {args.t}-of-{args.n}, {args.dvs}-DV shard per GPU of the 1M-DV batch"),
-                   "partials_per_step_per_gpu": args.dvs * args.n, "parallelism": f"shard{ws}",
+        "config": {"workload": WORKLOADS[args.workload].format(dvs=args.dvs, inject=args.inject),
+                   "partials_per_step_per_gpu": int(len(b.identifiers)), "parallelism": f"shard{ws}",
                    "inflight_launches": args.inflight, "batches_per_launch": M,
                    "rlc_group": group_used,
                    "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
@@ -434,9 +451,10 @@ def main():
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),
         "api_pipeline": api,
-        "isolated_batch_ms": {k: round(v, 3) for k, v in iso.items()},
+        "isolated_batch_ms": iso,
+        "isolated_kernel_ms": {k: round(v[0], 4) for k, v in sorted(kp.items(), key=lambda kv: -kv[1][0])
+                               if v[0] >= 0.05},
         "roofline": roofline,
-        "roofline_isolated": roofline_isolated,
         "roofline_pipeline": roofline_pipeline,
         "cpu_baseline": None,
         "host_signing_roots": None,
@@ -446,7 +464,7 @@ def main():
         # root (include/tbls_ssz.h), 16 threads -- must outpace `value`
         from tools.ssz_bench import run_rate
         result["host_signing_roots"] = run_rate(1 << 18, 16, reps=2)
-    if rank == 0 and not args.no_cpu and ws == 1:
+    if rank == 0 and not args.no_cpu and ws == 1 and args.workload in ("config2", "config3", "config4"):
         result["cpu_baseline"] = cpu_baseline(b, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result))

@@ -152,6 +152,10 @@ class TbgBatch(ctypes.Structure):
     ]
 
 
+class TbgKernelTime(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 64), ("ms", ctypes.c_float)]
+
+
 class TbgConfig(ctypes.Structure):
     _fields_ = [
         ("device", ctypes.c_int32),
@@ -194,6 +198,8 @@ SIGNATURES = {
                                 ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "tbg_submit_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    "tbg_replay_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                          ctypes.POINTER(ctypes.c_uint32)]),
     "tbg_replay_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                        ctypes.c_void_p]),
     "tbg_multi_init": (ctypes.c_int, [ctypes.POINTER(TbgConfig), ctypes.c_void_p, ctypes.c_uint32,

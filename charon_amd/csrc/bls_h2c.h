@@ -379,18 +379,26 @@ TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) {
 // g(x2) = Z^3 u^6 g(x1), so sqrt(g(x2)) = Z u^3 sqrt(Z g(x1)).
 // (The reference form tries sqrt(g(x1)), then sqrt(g(x2)): 1-2 roots and
 // an inversion per map, divergent across a wave.)
-TBG_NI void map_to_curve_g2_pair(const Fp2& u0, const Fp2& u1, G2J& q0, G2J& q1) {
+// In two halves around that inversion, so a kernel can batch it across its
+// workgroup (k_hash_map, bls_batchinv.h): sswu_pair_den forms the product dd
+// of the two denominators, sswu_pair_finish takes di = 1 / dd.
+struct SswuPair {
+  Fp2 zu2[2], den[2];
+};
+TBG_HD Fp2 sswu_pair_den(const Fp2& u0, const Fp2& u1, SswuPair& w) {
+  const Fp2 Z = fp2_from_const(SSWU_Z);
+  const Fp2* u[2] = {&u0, &u1};
+  for (int j = 0; j < 2; ++j) {
+    w.zu2[j] = fp2_reduce(fp2_mul(Z, fp2_sqr(*u[j])));
+    w.den[j] = fp2_reduce(fp2_add(fp2_sqr(w.zu2[j]), w.zu2[j]));
+  }
+  return fp2_reduce(fp2_mul(w.den[0], w.den[1]));
+}
+TBG_NI void sswu_pair_finish(const Fp2& u0, const Fp2& u1, const SswuPair& w, bool ok, const Fp2& di, G2J& q0,
+                             G2J& q1) {
   const Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B), Z = fp2_from_const(SSWU_Z);
   const Fp2* u[2] = {&u0, &u1};
-  Fp2 zu2[2], den[2];
-  for (int j = 0; j < 2; ++j) {
-    zu2[j] = fp2_reduce(fp2_mul(Z, fp2_sqr(*u[j])));
-    den[j] = fp2_reduce(fp2_add(fp2_sqr(zu2[j]), zu2[j]));
-  }
-  Fp2 dd = fp2_reduce(fp2_mul(den[0], den[1]));
-  bool ok = !fp2_is_zero(dd);
-  Fp2 di = fp2_inv(dd);
-  Fp2 inv[2] = {fp2_mul(den[1], di), fp2_mul(den[0], di)};
+  Fp2 inv[2] = {fp2_mul(w.den[1], di), fp2_mul(w.den[0], di)};
   G2J* out[2] = {&q0, &q1};
   for (int j = 0; j < 2 && ok; ++j) {
     Fp2 x1 = fp2_mul(fp2_from_const(SSWU_NEG_B_OVER_A), fp2_reduce(fp2_add(fp2_one(), inv[j])));
@@ -401,7 +409,7 @@ TBG_NI void map_to_curve_g2_pair(const Fp2& u0, const Fp2& u1, G2J& q0, G2J& q1)
       ok = false;
       break;
     }
-    Fp2 x = sq ? x1 : fp2_mul(zu2[j], x1);
+    Fp2 x = sq ? x1 : fp2_mul(w.zu2[j], x1);
     Fp2 y = sq ? r : fp2_mul(fp2_mul(Z, fp2_mul(fp2_sqr(*u[j]), *u[j])), r);
     if (fp2_sgn0(*u[j]) != fp2_sgn0(y)) y = fp2_reduce(fp2_neg(y));
     *out[j] = iso3_to_jac(x, y);
@@ -410,6 +418,12 @@ TBG_NI void map_to_curve_g2_pair(const Fp2& u0, const Fp2& u1, G2J& q0, G2J& q1)
     q0 = map_to_curve_g2(u0);
     q1 = map_to_curve_g2(u1);
   }
+}
+TBG_NI void map_to_curve_g2_pair(const Fp2& u0, const Fp2& u1, G2J& q0, G2J& q1) {
+  SswuPair w;
+  const Fp2 dd = sswu_pair_den(u0, u1, w);
+  const bool ok = !fp2_is_zero(dd);
+  sswu_pair_finish(u0, u1, w, ok, fp2_inv(dd), q0, q1);
 }
 
 // H(m) in G2 (Jacobian).  INL = true inlines the cofactor clearing's

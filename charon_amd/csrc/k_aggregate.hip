@@ -2,6 +2,7 @@
 // coefficients, G2 combination, affine conversion and 96-byte compression.
 #include "tbls_launch.h"
 #include "bls_tss.h"
+#include "bls_batchinv.h"
 
 namespace tbg {
 
@@ -41,17 +42,15 @@ __device__ void agg_emit(const DevBatch& B, uint32_t d, const G2J& acc) {
 // e.g. ids {1,2,4}: lambda_1 = 8/3) need a 255-bit [1/D] multiplication.
 // Inline, one such duty makes its whole 64-lane wave pay that loop; they are
 // listed here instead and finished by k_aggregate_finish in uniform waves.
-__global__ void TBG_LAUNCH k_aggregate(DevBatch B) {
-  uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= B.n_duties) return;
+// The affine conversion of the finished sums is batched over the workgroup
+// (bls_batchinv.h): every thread reaches it, with or without a sum to emit.
+__device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& emit) {
+  emit = false;
   uint8_t* out = B.agg + 96ull * d;
   for (int j = 0; j < 96; ++j) out[j] = 0;
   uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
   uint32_t n = last - first;
-  if (B.op == TBG_OP_VERIFY) {
-    B.duty_status[d] = TBG_DS_NOT_AGGREGATED;
-    return;
-  }
+  if (B.op == TBG_OP_VERIFY) return TBG_DS_NOT_AGGREGATED;
   int k = 0;
   bool decode_err = false, identity = false;
   for (uint32_t j = first; j < last; ++j) {
@@ -62,33 +61,56 @@ __global__ void TBG_LAUNCH k_aggregate(DevBatch B) {
   }
   if (B.op == TBG_OP_VERIFY_AGGREGATE) {
     uint32_t t = B.duty_threshold[d];
-    if (n < t) { B.duty_status[d] = TBG_DS_INSUFFICIENT; return; }
-    if ((uint32_t)k < t) { B.duty_status[d] = TBG_DS_INSUFFICIENT_VALID; return; }
+    if (n < t) return TBG_DS_INSUFFICIENT;
+    if ((uint32_t)k < t) return TBG_DS_INSUFFICIENT_VALID;
   } else {
-    if (decode_err) { B.duty_status[d] = TBG_DS_DECODE; return; }
-    if (identity) { B.duty_status[d] = TBG_DS_AGG_IDENTITY; return; }
+    if (decode_err) return TBG_DS_DECODE;
+    if (identity) return TBG_DS_AGG_IDENTITY;
   }
-  if (k < 2) { B.duty_status[d] = TBG_DS_AGG_TOO_FEW; return; }
+  if (k < 2) return TBG_DS_AGG_TOO_FEW;
   // duplicate identifiers among participants
   for (uint32_t a = first; a < last; ++a) {
     if (!participates(B.op, B.partial_status[a])) continue;
     for (uint32_t b = a + 1; b < last; ++b) {
-      if (participates(B.op, B.partial_status[b]) && B.identifiers[a] == B.identifiers[b]) {
-        B.duty_status[d] = TBG_DS_AGG_DUPLICATE_ID;
-        return;
-      }
+      if (participates(B.op, B.partial_status[b]) && B.identifiers[a] == B.identifiers[b])
+        return TBG_DS_AGG_DUPLICATE_ID;
     }
   }
   uint8_t mask[256];
   for (uint32_t j = first; j < last; ++j) mask[j - first] = participates(B.op, B.partial_status[j]) ? 1 : 0;
   uint64_t D = 1;
-  G2J acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
+  acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
   if (D > 1) {
     B.agg_acc[d] = acc;
     B.agg_list[atomicAdd(&B.counters[CNT_AGG], 1u)] = d;
+    return TBG_DS_OK;  // (k_aggregate_finish emits it)
+  }
+  emit = true;
+  return TBG_DS_OK;
+}
+
+__global__ void __launch_bounds__(BINV_BLOCK) k_aggregate(DevBatch B) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = d < B.n_duties;
+  G2J acc = jac_inf<Fp2>();
+  bool emit = false;
+  int32_t st = in ? agg_prepare(B, d, acc, emit) : TBG_DS_OK;
+  G2A a;
+  const bool aff = block_jac_to_aff<BINV_WAVES>(acc, emit, a);  // every thread of the workgroup
+  if (!in) return;
+  if (!emit) {
+    if (st != TBG_DS_OK) B.duty_status[d] = st;  // listed D > 1 duties: k_aggregate_finish sets it
     return;
   }
-  agg_emit(B, d, acc);
+  if (!aff) {
+    B.duty_status[d] = TBG_DS_AGG_IDENTITY;
+    return;
+  }
+  uint8_t enc[96];
+  g2_compress(a, false, enc);
+  uint8_t* out = B.agg + 96ull * d;
+  for (int j = 0; j < 96; ++j) out[j] = enc[j];
+  B.duty_status[d] = TBG_DS_OK;
 }
 
 __device__ __forceinline__ G2J shfl_xor_g2j(const G2J& a, int m) {
@@ -131,7 +153,8 @@ void launch_lagrange(const DevBatch& B, hipStream_t st) {
   if (B.n_partials) TBG_KLAUNCH(k_lagrange, grid_for(B.n_partials), dim3(kBlock), st, B);
 }
 void launch_aggregate(const DevBatch& B, hipStream_t st) {
-  if (B.n_duties) TBG_KLAUNCH(k_aggregate, grid_for(B.n_duties), dim3(kBlock), st, B);
+  if (B.n_duties)
+    TBG_KLAUNCH(k_aggregate, dim3((B.n_duties + BINV_BLOCK - 1) / BINV_BLOCK), dim3(BINV_BLOCK), st, B);
 }
 void launch_aggregate_finish(const DevBatch& B, hipStream_t st) {
   if (B.n_duties) TBG_KLAUNCH(k_aggregate_finish, grid_for(4 * B.n_duties), dim3(kBlock), st, B);

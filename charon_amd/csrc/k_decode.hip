@@ -9,21 +9,30 @@
 #include "tbls_launch.h"
 #include "bls_curve.h"
 #include "bls_pair.h"
+#include "bls_batchinv.h"
 
 namespace tbg {
 
 // Resident table entry: the key and [x]key (x the curve parameter), so the
 // RLC scalars of k_rlc.hip can be applied in base-x digits with the G1
 // endomorphism ([x^2] = -phi on G1) instead of 64-bit double-and-add.
-__global__ void TBG_LAUNCH k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x,
-                                                       int32_t* status) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t b[48];
-  for (int j = 0; j < 48; ++j) b[j] = pk48[48ull * i + j];
-  G1A a, ax;
-  int32_t st = g1_decompress(b, a);
-  if (st != DEC_OK || !jac_to_aff(jac_neg(jac_mul_xabs(jac_from_aff(a))), ax)) {
+// ([x]key's affine conversion batched over the workgroup, bls_batchinv.h)
+__global__ void __launch_bounds__(BINV_BLOCK) k_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x,
+                                                               int32_t* status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < n;
+  G1A a{fp_zero(), fp_zero()}, ax = a;
+  int32_t st = DEC_ERR_FLAGS;
+  G1J xa = jac_inf<Fp>();
+  if (in) {
+    uint8_t b[48];
+    for (int j = 0; j < 48; ++j) b[j] = pk48[48ull * i + j];
+    st = g1_decompress(b, a);
+    if (st == DEC_OK) xa = jac_neg(jac_mul_xabs(jac_from_aff(a)));
+  }
+  const bool ok = block_jac_to_aff<BINV_WAVES>(xa, in && st == DEC_OK, ax);  // every thread of the workgroup
+  if (!in) return;
+  if (st != DEC_OK || !ok) {
     if (st == DEC_OK) st = DEC_IDENTITY;  // unreachable for a prime-order point
     a.x = fp_zero();
     a.y = fp_zero();
@@ -81,7 +90,8 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_subgroup_sigs(DevBatch B) {
 }
 
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st) {
-  if (n) TBG_KLAUNCH(k_decode_pubkeys, grid_for(n), dim3(kBlock), st, pk48, n, out, out_x, status);
+  if (n) TBG_KLAUNCH(k_decode_pubkeys, dim3((n + BINV_BLOCK - 1) / BINV_BLOCK), dim3(BINV_BLOCK), st, pk48, n, out,
+                     out_x, status);
 }
 void launch_decode_sigs(const DevBatch& B, hipStream_t st) {
   // at least enough lanes to zero the counters (and level 0's bucket sizes)

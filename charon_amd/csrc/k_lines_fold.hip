@@ -16,19 +16,21 @@ namespace tbg {
 
 template <int KIND>
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
-  const uint32_t k = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
+  // both lanes of a pair take the same branches; the fallback kinds run in
+  // passes of fb_window list positions from fb_base (launch_rlc_check)
+  const uint32_t k = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + (KIND == FOLD_GROUPS || KIND == FOLD_L0 ? 0u : B.fb_base);
   uint32_t* out;
   if (KIND == FOLD_GROUPS) {
     if (k >= (B.n_duties + B.rlc_group - 1) / B.rlc_group || B.grp_state[k] != GRP_LINES) return;
     out = B.grp_lines;
   } else if (KIND == FOLD_CHUNKS) {
-    if (k >= B.counters[CNT_CHUNKS] || (B.chunk_list[k] & CHUNK_DEGENERATE)) return;
+    if (k >= B.counters[CNT_CHUNKS] || !fb_in_pass(B, k) || (B.chunk_list[k] & CHUNK_DEGENERATE)) return;
     out = B.chunk_lines;
   } else if (KIND == FOLD_CID) {
-    if (k >= B.counters[CNT_CID] || (B.cid_list[k] & ID_DEGENERATE)) return;
+    if (k >= B.counters[CNT_CID] || !fb_in_pass(B, k) || (B.cid_list[k] & ID_DEGENERATE)) return;
     out = B.cid_lines;
   } else if (KIND == FOLD_IDENT) {
-    if (k >= B.counters[CNT_DUTIES] || (B.id_list[k] & ID_DEGENERATE)) return;
+    if (k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k) || (B.id_list[k] & ID_DEGENERATE)) return;
     out = B.id_lines;
   } else {  // FOLD_L0: level 0's S (k_msm_sum)
     if (k != 0 || B.counters[CNT_L0_BAD]) return;
@@ -37,7 +39,8 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
     return;
   }
   const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  px_g2_lines(px_load(B.pend_pts[k]), nx, fp_from_const(G1_NEG_Y), out + (size_t)LINES_WORDS * k);
+  px_g2_lines(px_load(B.pend_pts[k]), nx, fp_from_const(G1_NEG_Y),
+              out + (KIND == FOLD_GROUPS ? (size_t)LINES_WORDS * k : fb_slot(B, k)));
 }
 
 void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStream_t st) {

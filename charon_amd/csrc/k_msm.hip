@@ -25,18 +25,27 @@
 #include "tbls_launch.h"
 #include "bls_msm.h"
 #include "bls_pair.h"
+#include "bls_batchinv.h"
 
 namespace tbg {
 
-// Pair table of every usable key (k_rlc_g1_l0): A+ = pk + [x]pk, A- = pk - [x]pk.
-__global__ void TBG_LAUNCH k_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab) {
+// Pair table of every usable key (k_rlc_g1_l0): A+ = pk + [x]pk, A- = pk - [x]pk
+// (the slope's inversion batched over the workgroup, bls_batchinv.h).
+__global__ void __launch_bounds__(BINV_BLOCK) k_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status,
+                                                              uint32_t n, G1A* tab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  G1A ap{fp_zero(), fp_zero()}, am = ap;
-  if (status[i] == DEC_OK) {
-    const G1A p0 = pk[i], x0 = xpk[i];
-    rlc_pair_from_inv(p0, x0, fp_inv(fp_reduce(fp_sub(x0.x, p0.x))), ap, am);
+  const bool in = i < n;
+  const bool ok = in && status[i] == DEC_OK;
+  G1A p0{fp_zero(), fp_zero()}, x0 = p0;
+  if (ok) {
+    p0 = pk[i];
+    x0 = xpk[i];
   }
+  // x0.x != p0.x for a prime-order key ([x]pk = +-pk would need x = +-1 mod r)
+  const Fp t = block_batch_inv<BINV_WAVES>(fp_reduce(fp_sub(x0.x, p0.x)), ok);  // every thread of the workgroup
+  if (!in) return;
+  G1A ap{fp_zero(), fp_zero()}, am = ap;
+  if (ok) rlc_pair_from_inv(p0, x0, t, ap, am);
   tab[2ull * i] = ap;
   tab[2ull * i + 1] = am;
 }
@@ -183,7 +192,8 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_sum(DevBatch B, const G2J* in
 }
 
 void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab, hipStream_t st) {
-  if (n) TBG_KLAUNCH(k_pubkey_tables, grid_for(n), dim3(kBlock), st, pk, xpk, status, n, tab);
+  if (n) TBG_KLAUNCH(k_pubkey_tables, dim3((n + BINV_BLOCK - 1) / BINV_BLOCK), dim3(BINV_BLOCK), st, pk, xpk, status, n,
+                     tab);
 }
 
 // Level 0 up to S's lines: G1 products and P_d (k_rlc_duty_sum), then the MSM.

@@ -3,9 +3,8 @@
 // (bls_pair.h: halves the G2 state per lane so the kernel fits two waves per
 // SIMD, which on gfx950 issue the multiply-adds ~1.7x faster than one).
 //
-//   phase 1, lane L owns partial L: one field inversion shared by both pair
-//            tables (Montgomery's trick, as the fused single-lane kernel did),
-//            then the whole G1 product on the lane;
+//   phase 1, lane L owns partial L: the G1 product from the key's pair
+//            table, the G2 table's slope inversion batched over the workgroup;
 //   phase 2, lanes (2k, 2k+1) run the G2 table and its 15 doublings + 31
 //            additions for partial 2k, then for 2k+1, with the Fp2
 //            coordinates split over the pair and the owner's inverse and
@@ -21,6 +20,7 @@
 #include "tbls_launch.h"
 #include "bls_rlc.h"
 #include "bls_pair.h"
+#include "bls_batchinv.h"
 
 namespace tbg {
 
@@ -56,10 +56,16 @@ __device__ __forceinline__ uint32_t u32_from_owner(uint32_t own, uint32_t j) {
   return pair_par() == j ? own : recv;
 }
 
-__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_rlc_partial2(DevBatch B, const G1A* pk_aff, const G1A* xpk_aff,
-                                                             const int32_t* pk_status, uint32_t n_pk) {
-  // No early return: both lanes of every pair must reach the DPP exchanges
-  // (the level-0 pass below is grid-uniform).
+// The G1 product comes from the key's pair table (k_pubkey_tables, computed
+// once per key) -- or was already formed by level 0 (k_rlc_g1_l0, same r_i)
+// when this runs after a level-0 failure; the G2 table's slope inversion is
+// batched over the workgroup (bls_batchinv.h).
+__global__ void __launch_bounds__(BINV_BLOCK, TBG_PAIR_WAVES) k_rlc_partial2(DevBatch B, const G1A* pk_tab,
+                                                                             const G1A* pk_aff,
+                                                                             const int32_t* pk_status, uint32_t n_pk) {
+  // No early return: both lanes of every pair must reach the DPP exchanges and
+  // every thread the workgroup's batched inversion (the level-0 pass below is
+  // grid-uniform).
   if (B.counters[CNT_L0_OK]) return;  // level 0 accepted the batch: no group levels
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool active = i < B.n_partials && B.partial_status[i] == TBG_PS_NOT_VERIFIED;
@@ -74,25 +80,17 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_rlc_partial2(DevBatch B, const G1
   const bool lead = active && rlc_group_lead(B, i, pk_status, n_pk);
   const bool work = active && !lead;
   uint32_t a[4] = {0, 0, 0, 0};
-  Fp2 inv2 = fp2_zero();
+  Fp2 dx2 = fp2_one();
   if (lead) {
     B.part_s[i] = jac_from_aff(B.sig_aff[i]);
     B.part_p[i] = jac_from_aff(pk_aff[pid]);
   } else if (work) {
     rlc_digits(rlc_scalar(B.rlc_seed, i), a);
     const G2A s = B.sig_aff[i];
-    const G1A p0 = pk_aff[pid], x0 = xpk_aff[pid];
-    // 1 / (psi(s).x - s.x) and 1 / ([x]pk.x - pk.x) from ONE inversion
-    const Fp2 dx2 = fp2_reduce(fp2_sub(fp2_mul(fp2_conj(s.x), fp2_from_const(PSI_X)), s.x));
-    const Fp dx1 = fp_reduce(fp_sub(x0.x, p0.x));
-    const Fp n2 = fp_mul2(dx2.c0, dx2.c0, dx2.c1, dx2.c1);
-    const Fp t = fp_inv(fp_mul(n2, dx1));
-    const Fp in2 = fp_mul(t, dx1);
-    inv2 = Fp2{fp_mul(dx2.c0, in2), fp_mul(fp_neg(dx2.c1), in2)};
-    G1A ap, am;
-    rlc_pair_from_inv(p0, x0, fp_mul(t, n2), ap, am);
-    B.part_p[i] = rlc_mul_table(ap, am, fp_from_const(G1_BETA), a);
+    dx2 = fp2_reduce(fp2_sub(fp2_mul(fp2_conj(s.x), fp2_from_const(PSI_X)), s.x));  // psi(s).x - s.x
+    if (!B.rlc_batch) B.part_p[i] = rlc_mul_table(pk_tab[2ull * pid], pk_tab[2ull * pid + 1], fp_from_const(G1_BETA), a);
   }
+  const Fp2 inv2 = block_batch_inv2<BINV_WAVES>(dx2, work);  // every thread of the workgroup
   for (uint32_t j = 0; j < 2; ++j) {
     if (!u32_from_owner(work ? 1u : 0u, j)) continue;  // pair-uniform
     const uint32_t owner = (i & ~1u) | j;
@@ -108,10 +106,11 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_rlc_partial2(DevBatch B, const G1
   }
 }
 
-void launch_rlc_partials(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status,
+void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st) {
   if (!B.n_partials) return;
-  TBG_KLAUNCH(k_rlc_partial2, grid_for(B.n_partials), dim3(kBlock), st, B, pk_aff, xpk_aff, pk_status, n_pk);
+  TBG_KLAUNCH(k_rlc_partial2, dim3((B.n_partials + BINV_BLOCK - 1) / BINV_BLOCK), dim3(BINV_BLOCK), st, B, pk_tab,
+              pk_aff, pk_status, n_pk);
 }
 
 }  // namespace tbg

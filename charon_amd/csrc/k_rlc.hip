@@ -35,6 +35,7 @@
 #include "bls_lines.h"
 #include "bls_quad.h"
 #include "bls_rlc.h"
+#include "bls_batchinv.h"
 
 namespace tbg {
 
@@ -59,11 +60,14 @@ __device__ __forceinline__ bool rlc_candidate(const DevBatch& B, uint32_t i) {
 // duty it cannot combine (P_d = 0) makes level 0 fail; after a level-0
 // failure DSUM_FALLBACK_S adds the S_d of the duties level 0 combined (the
 // stored P-chunk products include them; S_d = 0 is just a term of the sums).
-__global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B, int phase) {
-  uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= B.n_duties) return;
-  if (phase == DSUM_FALLBACK_S) {
-    if (B.counters[CNT_L0_OK] || B.dv_state[d] != RLC_COMBINED) return;
+// P_d's affine conversion is batched over the workgroup (bls_batchinv.h).
+template <int PHASE>
+__global__ void __launch_bounds__(BINV_BLOCK) k_rlc_duty_sum(DevBatch B) {
+  constexpr int phase = PHASE;
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = d < B.n_duties;
+  if (phase == DSUM_FALLBACK_S) {  // (no inversion: no workgroup-wide step)
+    if (!in || B.counters[CNT_L0_OK] || B.dv_state[d] != RLC_COMBINED) return;
     G2J S = jac_inf<Fp2>();
     for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i)
       if (rlc_candidate(B, i)) S = jac_add(S, B.part_s[i]);
@@ -73,18 +77,22 @@ __global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B, int phase) {
   G1J P = jac_inf<Fp>();
   G2J S = jac_inf<Fp2>();
   int cand = 0;
-  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) {
-    if (!rlc_candidate(B, i)) continue;
-    P = jac_add(P, B.part_p[i]);
-    if (phase == DSUM_BOTH) S = jac_add(S, B.part_s[i]);
-    ++cand;
+  if (in) {
+    for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) {
+      if (!rlc_candidate(B, i)) continue;
+      P = jac_add(P, B.part_p[i]);
+      if (phase == DSUM_BOTH) S = jac_add(S, B.part_s[i]);
+      ++cand;
+    }
   }
+  G1A Pa;
+  const bool aff = block_jac_to_aff<BINV_WAVES>(P, cand > 0, Pa);  // every thread of the workgroup
+  if (!in) return;
   if (cand == 0) {
     B.dv_state[d] = RLC_NONE;
     return;
   }
-  G1A Pa;
-  if (!jac_to_aff(P, Pa) || (phase == DSUM_BOTH && jac_is_inf(S))) {
+  if (!aff || (phase == DSUM_BOTH && jac_is_inf(S))) {
     B.dv_state[d] = RLC_EACH;  // degenerate combination: check the partials one by one
     if (phase == DSUM_L0_P) B.counters[CNT_L0_BAD] = 1;
     return;
@@ -93,6 +101,7 @@ __global__ void TBG_LAUNCH k_rlc_duty_sum(DevBatch B, int phase) {
   if (phase == DSUM_BOTH) B.dv_s[d] = S;
   B.dv_state[d] = RLC_COMBINED;
 }
+inline dim3 duty_grid(const DevBatch& B) { return dim3((B.n_duties + BINV_BLOCK - 1) / BINV_BLOCK); }
 
 // One thread per group: S = sum of the group's S_d, affine (its Miller lines,
 // -g1 folded in: k_lines_fold.hip).
@@ -174,7 +183,11 @@ __device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
 //   MILLER_L0       P chunks, then ONE quad for level 0's S (batch_f);
 //   MILLER_GROUP_S  after a level-0 failure: the groups' S quads only (the P
 //                   chunk products of level 0 serve the group checks as they are).
-__global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B, int mode) {
+// (a template on the mode: each mode is its own kernel symbol, so per-kernel
+// profiles separate level 0's P chunks from the fallback-only S quads)
+template <int MODE>
+__global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
+  constexpr int mode = MODE;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
@@ -436,8 +449,8 @@ __device__ __forceinline__ void resolve_bad_duty(const DevBatch& B, uint32_t d, 
 // go to level 1.5b with the chunk's value (a degenerate S_c: level 3).
 __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = fp12_slot(t);
-  if (k >= B.counters[CNT_CHUNKS]) return;
+  uint32_t k = fp12_slot(t) + B.fb_base;  // (fp12_slot's idle-lane value stays out of range)
+  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_CHUNKS] || !fb_in_pass(B, k)) return;
   const bool lead = quad_lane() == 0;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C, nq = nch + 1;
   const uint32_t entry = B.chunk_list[k], qc = entry & ~CHUNK_DEGENERATE, g = qc / nch, c = qc % nch;
@@ -448,7 +461,7 @@ __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
         if (rlc_combinable(B, d)) rlc_push_partials(B, d);
     return;
   }
-  const uint32_t* ls = B.chunk_lines + (size_t)LINES_WORDS * k;
+  const uint32_t* ls = B.chunk_lines + fb_slot(B, k);
   Fp4 f = quad_one();
   int idx = 0;
   for (int b = 62; b >= 0; --b) {
@@ -512,8 +525,8 @@ __global__ void TBG_LAUNCH k_rlc_cident_lines(DevBatch B) {
 // chunk's candidates go to level 3.
 __global__ void TBG_LAUNCH k_rlc_cident_check(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t j = fp12_slot(t);
-  if (j >= B.counters[CNT_CID]) return;
+  uint32_t j = fp12_slot(t) + B.fb_base;
+  if (fp12_slot(t) == 0xFFFFFFFFu || j >= B.counters[CNT_CID] || !fb_in_pass(B, j)) return;
   const bool lead = quad_lane() == 0;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C;
   const uint32_t entry = B.cid_list[j], k = entry & ~ID_DEGENERATE;
@@ -523,7 +536,7 @@ __global__ void TBG_LAUNCH k_rlc_cident_check(DevBatch B) {
   for (uint32_t d = d0; d < d1; ++d) n += rlc_combinable(B, d) ? 1u : 0u;
   const Fp4 A = quad_load(B.chunk_fe + (size_t)3 * QUAD_WORDS * k);
   if (!(entry & ID_DEGENERATE)) {
-    const uint32_t* ls = B.cid_lines + (size_t)LINES_WORDS * j;
+    const uint32_t* ls = B.cid_lines + fb_slot(B, j);
     const G1A* wp = B.cid_p + (size_t)C * j;
     Fp4 f = quad_one();
     int idx = 0;
@@ -592,15 +605,15 @@ __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
 // Found -> partial w invalid, the others valid; not found -> level 3.
 __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = fp12_slot(t);
-  if (k >= B.counters[CNT_DUTIES]) return;
+  uint32_t k = fp12_slot(t) + B.fb_base;
+  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k)) return;
   const bool lead = quad_lane() == 0;
   const uint32_t entry = B.id_list[k], d = entry & ~ID_DEGENERATE;
   uint32_t found = 0;
   if (!(entry & ID_DEGENERATE)) {
     const G1A P = B.id_p[k];
     Fp nx = fp_reduce(fp_neg(P.x));
-    const uint32_t* ls = B.id_lines + (size_t)LINES_WORDS * k;
+    const uint32_t* ls = B.id_lines + fb_slot(B, k);
     const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d];
     Fp4 f = quad_one();
     int idx = 0;
@@ -651,18 +664,18 @@ __global__ void TBG_LAUNCH k_list_all_partials(DevBatch B, const int32_t* pk_sta
 
 // Level 3 lines: one thread per listed partial, lines of its signature.
 __global__ void TBG_LAUNCH k_lines_sig_list(DevBatch B) {
-  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= B.counters[CNT_PARTIALS]) return;
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x + B.fb_base;
+  if (k >= B.counters[CNT_PARTIALS] || !fb_in_pass(B, k)) return;
   uint32_t i = B.part_list[k];
   Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines_t<true>(B.sig_aff[i], nx, fp_from_const(G1_NEG_Y), B.sig_lines + (size_t)LINES_WORDS * k);
+  g2_lines_t<true>(B.sig_aff[i], nx, fp_from_const(G1_NEG_Y), B.sig_lines + fb_slot(B, k));
 }
 
 // Level 3 check: one quad per listed partial, the exact CoreVerify.
 __global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = fp12_slot(t);
-  if (k >= B.counters[CNT_PARTIALS]) return;
+  uint32_t k = fp12_slot(t) + B.fb_base;
+  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_PARTIALS] || !fb_in_pass(B, k)) return;
   const bool lead = quad_lane() == 0;
   uint32_t i = B.part_list[k];
   uint32_t m = B.duty_msg[B.partial_duty[i]];
@@ -672,7 +685,7 @@ __global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   }
   G1A pk = pk_aff[B.pubkey_ids[i]];
   Fp nx = fp_reduce(fp_neg(pk.x));
-  const uint32_t* ls = B.sig_lines + (size_t)LINES_WORDS * k;
+  const uint32_t* ls = B.sig_lines + fb_slot(B, k);
   const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * m;
   Fp4 f = quad_one();
   int idx = 0;
@@ -689,6 +702,18 @@ __global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   if (lead) B.partial_status[i] = ok ? TBG_PS_VALID : TBG_PS_INVALID;
 }
 
+// The fallback levels' list positions [0, max_entries) in passes of
+// B.fb_window (the line buffer's capacity; 0: one pass), in stream order.
+template <class F>
+static void fb_passes(const DevBatch& B, uint32_t max_entries, F&& body) {
+  const uint32_t W = B.fb_window ? B.fb_window : max_entries;
+  for (uint32_t base = 0; base < max_entries; base += W) {
+    DevBatch P = B;
+    P.fb_base = base;
+    body(P, max_entries - base < W ? max_entries - base : W);
+  }
+}
+
 void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const G1A* pk_tab,
                         const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
   if (!B.n_duties) return;
@@ -699,12 +724,12 @@ void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff
   uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
   if (B.rlc_batch) {  // level 0: G1 products, P_d, the signature MSM and S's lines
     launch_l0_prepare(B, pk_tab, pk_status, n_pk, st);
-    TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B, (int)DSUM_L0_P);
+    TBG_KLAUNCH(k_rlc_duty_sum<DSUM_L0_P>, duty_grid(B), dim3(BINV_BLOCK), st, B);
     launch_lines_fold(B, FOLD_L0, 1, st);
     return;
   }
-  launch_rlc_partials(B, pk_aff, xpk_aff, pk_status, n_pk, st);
-  TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B, (int)DSUM_BOTH);
+  launch_rlc_partials(B, pk_tab, pk_aff, pk_status, n_pk, st);
+  TBG_KLAUNCH(k_rlc_duty_sum<DSUM_BOTH>, duty_grid(B), dim3(BINV_BLOCK), st, B);
   TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
   launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
 }
@@ -717,7 +742,7 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
     if (B.rlc_batch) {
       // level 0: the P chunks (kept for the group levels) and S, one product
-      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(fp12_threads((n_groups * nch + 1))), dim3(kBlock), st, B, (int)MILLER_L0);
+      TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_L0>, grid_for(fp12_threads((n_groups * nch + 1))), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_l0_fold, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
       uint32_t in = 0, n = n_groups, out = n_groups;
       while (n > L0_TREE_FAN) {
@@ -731,31 +756,39 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
       TBG_KLAUNCH(k_l0_after, grid_for(n_groups), dim3(kBlock), st, B);
       // level 0 failed: the group levels' signature side (these kernels
       // return at once after a pass)
-      launch_rlc_partials(B, pk_aff, xpk_aff, pk_status, n_pk, st);
-      TBG_KLAUNCH(k_rlc_duty_sum, grid_for(B.n_duties), dim3(kBlock), st, B, (int)DSUM_FALLBACK_S);
+      launch_rlc_partials(B, nullptr, pk_aff, pk_status, n_pk, st);  // (G1 products: level 0's)
+      TBG_KLAUNCH(k_rlc_duty_sum<DSUM_FALLBACK_S>, duty_grid(B), dim3(BINV_BLOCK), st, B);
       TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
       launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
-      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B, (int)MILLER_GROUP_S);
+      TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_GROUP_S>, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
     } else {
-      TBG_KLAUNCH(k_rlc_miller_chunks, grid_for(fp12_threads(n_groups * (nch + 1))), dim3(kBlock), st, B, (int)MILLER_GROUPS);
+      TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_GROUPS>, grid_for(fp12_threads(n_groups * (nch + 1))), dim3(kBlock), st, B);
     }
     TBG_KLAUNCH(k_rlc_group_final, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
       TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
-      launch_lines_fold(B, FOLD_CHUNKS, n_groups * nch, st);
-      TBG_KLAUNCH(k_rlc_check_chunks, grid_for(fp12_threads(n_groups * nch)), dim3(kBlock), st, B);
+      fb_passes(B, n_groups * nch, [&](const DevBatch& P, uint32_t n) {
+        launch_lines_fold(P, FOLD_CHUNKS, n, st);
+        TBG_KLAUNCH(k_rlc_check_chunks, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+      });
       TBG_KLAUNCH(k_rlc_cident_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
-      launch_lines_fold(B, FOLD_CID, n_groups * nch, st);
-      TBG_KLAUNCH(k_rlc_cident_check, grid_for(fp12_threads(n_groups * nch)), dim3(kBlock), st, B);
+      fb_passes(B, n_groups * nch, [&](const DevBatch& P, uint32_t n) {
+        launch_lines_fold(P, FOLD_CID, n, st);
+        TBG_KLAUNCH(k_rlc_cident_check, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+      });
       TBG_KLAUNCH(k_rlc_ident_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
-      launch_lines_fold(B, FOLD_IDENT, B.n_duties, st);
-      TBG_KLAUNCH(k_rlc_ident_check, grid_for(fp12_threads(B.n_duties)), dim3(kBlock), st, B);
+      fb_passes(B, B.n_duties, [&](const DevBatch& P, uint32_t n) {
+        launch_lines_fold(P, FOLD_IDENT, n, st);
+        TBG_KLAUNCH(k_rlc_ident_check, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+      });
     }
   }
   if (B.n_partials) {
-    TBG_KLAUNCH(k_lines_sig_list, grid_for(B.n_partials), dim3(kBlock), st, B);
-    TBG_KLAUNCH(k_verify_list, grid_for(fp12_threads(B.n_partials)), dim3(kBlock), st, B, pk_aff);
+    fb_passes(B, B.n_partials, [&](const DevBatch& P, uint32_t n) {
+      TBG_KLAUNCH(k_lines_sig_list, grid_for(n), dim3(kBlock), st, P);
+      TBG_KLAUNCH(k_verify_list, grid_for(fp12_threads(n)), dim3(kBlock), st, P, pk_aff);
+    });
   }
 }
 

@@ -30,6 +30,23 @@ void debug_after_launch(const char* kernel, hipStream_t st) {
   (void)hipEventDestroy(a);
   fprintf(stderr, "[tbg] %s done: %s\n", kernel, hipGetErrorString(e));
 }
+
+struct KProfRec {
+  const char* name;
+  hipEvent_t a, b;
+};
+static thread_local std::vector<KProfRec>* g_kprof = nullptr;
+void kprof_pre(const char* kernel, hipStream_t st) {
+  if (!g_kprof) return;
+  KProfRec r{kernel, nullptr, nullptr};
+  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return;
+  (void)hipEventRecord(r.a, st);
+  g_kprof->push_back(r);
+}
+void kprof_post(hipStream_t st) {
+  if (!g_kprof || g_kprof->empty()) return;
+  (void)hipEventRecord(g_kprof->back().b, st);
+}
 }  // namespace tbg
 
 namespace {
@@ -458,7 +475,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   }
   if (np64 > 0x7FFFFFFFull || nd64 > 0x7FFFFFFFull || nm64 > 0x7FFFFFFFull || mb64 > 0xFFFFFFFFull)
     return TBG_E_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::unique_lock<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   // Least recently used free slot: a collected batch stays resident (for
   // tbg_replay / tbg_fetch) until every other slot has been reused.
@@ -490,7 +507,11 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_h_st = sec(4ull * nm);
   size_t w_h_jac = sec(3 * sizeof(G2J) * (size_t)nm);  // H(m) + the cofactor clearing's two temporaries
   size_t w_lam = sec(32ull * np);
-  size_t w_sl = sec(verify ? 4ull * LINES_WORDS * np : 0);
+  // The fallback levels' lines share one buffer of fb_w list positions,
+  // consumed in passes (DevBatch::fb_window): a slot no longer holds 22.8 KB
+  // per partial for lists that a clean batch leaves empty.
+  const uint32_t fb_w = verify ? std::max<uint32_t>(1u, std::min<uint32_t>(TBG_FB_WINDOW, np)) : 0u;
+  size_t w_sl = sec(4ull * LINES_WORDS * fb_w);
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
   if (c->rlc_auto)
     c->rlc_group = c->invalid_ema < TBG_RLC_AUTO_TO8 ? 16 : c->invalid_ema < TBG_RLC_AUTO_TO4 ? 8 : 4;
@@ -506,7 +527,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_ps = sec(G ? sizeof(G2J) * (size_t)np : 0);
   size_t w_cf = sec(G ? 4ull * 3 * 4 * NL * ng * (nch + 1) : 0);
   size_t w_cl = sec(G > 1 ? 4ull * ng * nch : 0);
-  size_t w_clines = sec(G > 1 ? 4ull * LINES_WORDS * ng * nch : 0);
+
   size_t w_dvp = sec(G ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_dvs = sec(G ? sizeof(G2J) * (size_t)nd : 0);
   size_t w_dvst = sec(G ? 4ull * nd : 0);
@@ -519,7 +540,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_cfe = sec(G > 1 ? 4ull * 3 * 4 * NL * ng * nch : 0);
   size_t w_cidl = sec(G > 1 ? 4ull * ng * nch : 0);
   size_t w_cidp = sec(G > 1 ? sizeof(G1A) * (size_t)ng * nch * C : 0);
-  size_t w_cidlines = sec(G > 1 ? 4ull * LINES_WORDS * ng * nch : 0);
+
   size_t w_idl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_idp = sec(G > 1 ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_mr = sec(l0 ? 8ull * np : 0);
@@ -546,6 +567,12 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   if ((rc = grow_pinned(&s->h_out, &s->h_out_cap, out_bytes)) != TBG_OK) return rc;
   if ((rc = grow_device(&s->d_in, &s->d_in_cap, in_bytes)) != TBG_OK) return rc;
   if ((rc = grow_device(&s->d_work, &s->d_work_cap, work_bytes)) != TBG_OK) return rc;
+  // Reserve the slot (busy, its old tickets expired) and pack WITHOUT the
+  // context lock: a 16-batch group is ~70 MB of host copies, during which
+  // other threads' tbg_poll / tbg_collect / tbg_submit must not wait.
+  s->parts.clear();
+  s->busy = true;
+  lk.unlock();
 
   // ---- pack: batch k's duties / partials / messages follow batch k-1's,
   // every index rebased by the running offsets ----
@@ -611,6 +638,13 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   duty_first[nd] = np;
   if (verify) msg_off[nm] = MB;
 
+  lk.lock();
+  // from here on a failure releases the reserved slot
+  auto release = [&](int code) {
+    s->busy = false;
+    return code;
+  };
+  if (hipSetDevice(c->device) != hipSuccess) return release(TBG_E_DEVICE);
   DevBatch B;
   memset(&B, 0, sizeof(B));
   B.op = op;
@@ -661,7 +695,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.part_s = (G2J*)(dw + w_ps);
   B.chunk_f = (uint32_t*)(dw + w_cf);
   B.chunk_list = (uint32_t*)(dw + w_cl);
-  B.chunk_lines = (uint32_t*)(dw + w_clines);
+  B.chunk_lines = B.sig_lines;  // (one fallback line buffer, see w_sl)
   B.dv_p = (G1A*)(dw + w_dvp);
   B.dv_s = (G2J*)(dw + w_dvs);
   B.dv_state = (int32_t*)(dw + w_dvst);
@@ -674,10 +708,12 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.chunk_fe = (uint32_t*)(dw + w_cfe);
   B.cid_list = (uint32_t*)(dw + w_cidl);
   B.cid_p = (G1A*)(dw + w_cidp);
-  B.cid_lines = (uint32_t*)(dw + w_cidlines);
+  B.cid_lines = B.sig_lines;
   B.id_list = (uint32_t*)(dw + w_idl);
   B.id_p = (G1A*)(dw + w_idp);
-  B.id_lines = B.sig_lines;  // nd <= np list positions; level 3 rewrites them after level 2b
+  B.id_lines = B.sig_lines;
+  B.fb_window = fb_w;
+  B.fb_base = 0;
   B.partial_status = (int32_t*)(dw + w_pst);
   B.duty_status = (int32_t*)(dw + w_dst);
   B.agg = dw + w_agg;
@@ -699,12 +735,14 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   hipStream_t st = s->st;
   // The resident pubkey table may have been (re)loaded on the utility stream
   // (already complete: tbg_load_pubkeys waits for it; ordered anyway).
-  HIP_TRY(hipStreamWaitEvent(st, c->keys_ready, 0));
-  HIP_TRY(hipMemcpyAsync(s->d_in, s->h_in, in_bytes, hipMemcpyHostToDevice, st));
+  if (hipStreamWaitEvent(st, c->keys_ready, 0) != hipSuccess ||
+      hipMemcpyAsync(s->d_in, s->h_in, in_bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+    return release(TBG_E_DEVICE);
   rc = launch_chain(c, *s, B, s->ev);
-  if (rc != TBG_OK) return rc;
-  HIP_TRY(hipMemcpyAsync(s->h_out, dw + w_out, out_bytes, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipEventRecord(s->done, st));
+  if (rc != TBG_OK) return release(rc);
+  if (hipMemcpyAsync(s->h_out, dw + w_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipEventRecord(s->done, st) != hipSuccess)
+    return release(TBG_E_DEVICE);
 
   for (uint32_t k = 0; k < n_batches; ++k) {
     parts[k].ticket = c->next_ticket++;
@@ -857,6 +895,41 @@ int tbg_replay_plan(tbg_ctx* c, const tbg_ticket* tickets, const uint32_t* n_par
     memcpy(c->last_ms, acc, sizeof(acc));
   }
   for (auto& e : ev) hipEventDestroy(e);
+  return rc;
+}
+
+int tbg_replay_profile(tbg_ctx* c, tbg_ticket t, tbg_kernel_time* out, uint32_t max_entries, uint32_t* n_entries) {
+  if (!c || !n_entries || (max_entries && !out)) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = find_ticket(c, t, false, nullptr);
+  if (!s) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  // nothing else of this context in flight: every kernel runs alone
+  for (auto& x : c->slots) {
+    HIP_TRY(hipStreamSynchronize(x.st));
+    HIP_TRY(hipStreamSynchronize(x.st2));
+  }
+  std::vector<KProfRec> rec;
+  hipEvent_t ev[kChainEvents];
+  for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  g_kprof = &rec;
+  int rc = launch_chain(c, *s, s->B, ev);
+  g_kprof = nullptr;
+  if (hipStreamSynchronize(s->st) != hipSuccess || hipStreamSynchronize(s->st2) != hipSuccess) rc = TBG_E_DEVICE;
+  uint32_t n = 0;
+  for (auto& r : rec) {
+    if (rc == TBG_OK && n < max_entries) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) rc = TBG_E_DEVICE;
+      snprintf(out[n].name, sizeof(out[n].name), "%s", r.name);
+      out[n].ms = ms;
+      ++n;
+    }
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  *n_entries = n;
   return rc;
 }
 

@@ -5,11 +5,17 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "bls_curve.h"
+#include "bls_lines.h"
 #include "../../include/tbls_gpu.h"
 
 namespace tbg {
 
 constexpr int kBlock = 64;
+// List positions per pass of the fallback levels' shared line buffer
+// (22.8 KB each: 0.75 GB per slot).
+#ifndef TBG_FB_WINDOW
+#define TBG_FB_WINDOW 32768u
+#endif
 
 // Minimum waves per SIMD requested from the register allocator (1 lets a
 // kernel use all 512 / 2 = 256 VGPRs at two waves per SIMD; 3 caps it at
@@ -52,7 +58,7 @@ struct DevBatch {
   G2J* h_jac;          // [3 n_msgs] H(m) before affine conversion (k_hash_map / _clear / _affine), then
                        // the cofactor clearing's temporaries [x]P and [x]P + psi(P) (k_hash_clear.hip)
   uint32_t* lam;       // [n_partials][8] scalar words
-  uint32_t* sig_lines;  // [n_partials][LINES_WORDS] Miller lines of listed signatures (-g1 folded in)
+  uint32_t* sig_lines;  // [fb window][LINES_WORDS] Miller lines of listed signatures (-g1 folded in)
   uint32_t* h_lines;    // [n_msgs][LINES_WORDS] Miller lines of each H(m) (G1 factor left out)
   // random-linear-combination verification (k_rlc.hip)
   uint32_t rlc_seed[8];   // secret per-batch key of the scalars r_i
@@ -63,7 +69,7 @@ struct DevBatch {
   uint32_t* chunk_f;      // [n_groups * (chunks + 1)][3][4 NL] Miller products of the chunks (quad layout);
                           // chunk index `chunks` of a group is its S pair alone
   uint32_t* chunk_list;   // [n_groups * chunks] level-1.5 chunks of failed groups (group * chunks + c)
-  uint32_t* chunk_lines;  // [n_groups * chunks][LINES_WORDS] lines of S_c, by chunk-list position
+  uint32_t* chunk_lines;  // [fb window][LINES_WORDS] lines of S_c, by chunk-list position - fb_base
   G1A* dv_p;              // [n_duties] sum r_i pk_i (affine)
   G2J* dv_s;              // [n_duties] sum r_i sig_i
   int32_t* dv_state;      // [n_duties] RLC_*
@@ -76,10 +82,17 @@ struct DevBatch {
   uint32_t* chunk_fe;     // [n_groups * chunks][3][4 NL] final-exponentiated value of failed chunks (by list position)
   uint32_t* cid_list;     // [n_groups * chunks] level-1.5b entries: chunk-list positions
   G1A* cid_p;             // [n_groups * chunks][rlc_chunk] w_d P_d as (-x, y), by level-1.5b position
-  uint32_t* cid_lines;    // [n_groups * chunks][LINES_WORDS] lines of sum w_d S_d, by level-1.5b position
+  uint32_t* cid_lines;    // [fb window][LINES_WORDS] lines of sum w_d S_d, by level-1.5b position - fb_base
   uint32_t* id_fe;        // [n_duties][3][4 NL] value A_d of each level-2b duty (by list position)
   uint32_t* id_list;      // [n_duties] level-2b entries: failed duties with several candidates
   G1A* id_p;              // [n_duties] sum w_i r_i pk_i (affine), by level-2b position
+  // The fallback levels' line buffers (chunk_lines, cid_lines, id_lines,
+  // sig_lines) are ONE buffer of fb_window entries (0: unbounded), used in
+  // stream order: each level's lines are written and consumed in passes of
+  // fb_window list positions [fb_base, fb_base + fb_window) before the next
+  // level writes (launch_rlc_check) -- a slot's HBM no longer scales with the
+  // worst-case list length (22.8 KB per partial of every batch).
+  uint32_t fb_window, fb_base;
   uint32_t* id_lines;     // lines of sum w_i r_i sig_i by level-2b position: aliases sig_lines,
                           // which level 3 only fills after level 2b has consumed them
   // level 0 (k_msm.hip, k_rlc.hip): the whole device batch as ONE RLC check,
@@ -140,6 +153,10 @@ constexpr uint32_t ID_DEGENERATE = 0x80000000u;
 // k_lines_fold<KIND>: which pending points get lines, and where they go.
 enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3, FOLD_L0 = 4 };
 
+// Fallback list position k in the current pass, and its slot in the line buffer.
+TBG_HD bool fb_in_pass(const DevBatch& B, uint32_t k) { return B.fb_window == 0 || k - B.fb_base < B.fb_window; }
+TBG_HD size_t fb_slot(const DevBatch& B, uint32_t k) { return (size_t)LINES_WORDS * (k - B.fb_base); }
+
 // Participation of a partial in its duty's aggregate.
 TBG_HD bool participates(uint32_t op, int32_t st) {
   return op == TBG_OP_VERIFY_AGGREGATE ? (st == TBG_PS_VALID) : (st == TBG_PS_NOT_VERIFIED);
@@ -149,9 +166,16 @@ TBG_HD bool participates(uint32_t op, int32_t st) {
 // followed by a stream synchronisation and a line on stderr (kernel, ms,
 // status), so a faulting or runaway kernel names itself.  Off by default.
 void debug_after_launch(const char* kernel, hipStream_t st);
+// Per-kernel timing (tbg_replay_profile): while a recorder is active on the
+// launching thread every launch is bracketed by a HIP event pair on its own
+// stream; otherwise these are a thread-local pointer test.
+void kprof_pre(const char* kernel, hipStream_t st);
+void kprof_post(hipStream_t st);
 #define TBG_KLAUNCH(kernel, grid, block, st, ...)                      \
   do {                                                                \
+    kprof_pre(#kernel, st);                                           \
     hipLaunchKernelGGL(kernel, grid, block, 0, st, __VA_ARGS__);      \
+    kprof_post(st);                                                   \
     debug_after_launch(#kernel, st);                                  \
   } while (0)
 
@@ -185,7 +209,8 @@ void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStr
 void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab, hipStream_t st);
 void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
 void launch_l0_check(const DevBatch& B, hipStream_t st);
-void launch_rlc_partials(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status,
+// pk_tab: the keys' pair tables (k_pubkey_tables); unused after a level-0 failure (level 0 formed the G1 products)
+void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);
 void launch_lagrange(const DevBatch& B, hipStream_t st);
 void launch_aggregate(const DevBatch& B, hipStream_t st);

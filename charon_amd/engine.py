@@ -200,6 +200,15 @@ class Engine:
         self._check(self._lib.tbg_replay_plan(self._h, _ptr(t), _ptr(p), len(t), _ptr(ms)), "tbg_replay_plan")
         return dict(zip(TIMING_KEYS, ms.tolist()))
 
+    def replay_profile(self, ticket, max_entries=512):
+        """Replay one resident device batch alone with an event pair around
+        every kernel (tbg_replay_profile): [(kernel, ms)] in launch order."""
+        buf = (_native.TbgKernelTime * max_entries)()
+        n = ctypes.c_uint32()
+        self._check(self._lib.tbg_replay_profile(self._h, ticket, buf, max_entries, ctypes.byref(n)),
+                    "tbg_replay_profile")
+        return [(buf[k].name.decode(), float(buf[k].ms)) for k in range(n.value)]
+
     def fetch(self, ticket, n_duties, n_partials) -> BatchResult:
         ps = np.zeros(n_partials, dtype=np.int32)
         ds = np.zeros(n_duties, dtype=np.int32)

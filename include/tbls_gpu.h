@@ -199,6 +199,17 @@ int tbg_replay_multi(tbg_ctx* ctx, const tbg_ticket* tickets, uint32_t n_tickets
  * that slot's streams; launches of different slots are in flight together. */
 int tbg_replay_plan(tbg_ctx* ctx, const tbg_ticket* tickets, const uint32_t* n_parts, uint32_t n_launches, float* ms8);
 int tbg_fetch(tbg_ctx* ctx, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status, uint8_t* agg96);
+/* Measurement hook (bench.py's roofline): replay one collected device batch
+ * ALONE (the context's other slots drained first) with a HIP event pair
+ * around every kernel launch on the stream it runs on; out[k] = the k-th
+ * launch's kernel name (as written at the launch site) and duration in ms,
+ * in launch order, at most max_entries of them.  Blocks. */
+typedef struct {
+  char name[64];
+  float ms;
+} tbg_kernel_time;
+int tbg_replay_profile(tbg_ctx* ctx, tbg_ticket ticket, tbg_kernel_time* out, uint32_t max_entries,
+                       uint32_t* n_entries);
 /* Verification work of a collected batch's last run: out4 = [level-1 groups,
  * failed duties searched for their invalid partial (level 2b), partials
  * checked one by one (level 3), duties per group (0 = TBG_VERIFY_EACH)]. */

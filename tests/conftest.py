@@ -11,3 +11,14 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: test needs an MI355X (runs the HIP engine)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+def progress(msg: str) -> None:
+    """A progress line for long GPU tests: appended to gpurun_out/progress.log
+    (the GPU box's watchdog sees files there change) and echoed to stderr."""
+    import time
+    d = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "progress.log"), "a") as f:
+        f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+    print(msg, file=sys.stderr, flush=True)

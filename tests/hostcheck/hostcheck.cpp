@@ -626,3 +626,120 @@ extern "C" int hc_h2f_check(const uint8_t* msg, uint32_t len) {
   hash_to_field_fp2_bytes(msg, len, b0, b1);
   return fp2_eq(a0, b0) && fp2_eq(a1, b1) ? 1 : 0;
 }
+
+// Per-kernel work probes (tools/count_work.py -> profiles/work_model.json
+// "kernels"): each runs the single-lane equivalent of ONE item of one kernel
+// of the level-0 chain, so bench.py can price the dominant kernel alone.
+extern "C" {
+// k_decode_sigs: flags, field, Fp2 square root (no subgroup check)
+int hc_k_decode_sigs(const uint8_t* sig96) {
+  G2A a;
+  return g2_decompress_t<true, false>(sig96, a);
+}
+// k_subgroup_sigs: psi(a) == [x] a on the decoded point
+int hc_k_subgroup_sigs(const uint8_t* sig96) {
+  G2A a;
+  if (g2_decompress_t<true, false>(sig96, a) != DEC_OK) return -1;
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  return g2_in_subgroup_aff_in(a) ? 1 : 0;
+}
+// k_hash_map: hash_to_field, both SSWU maps + isogenies, Q0 + Q1
+void hc_k_hash_map(const uint8_t* msg, uint32_t len) {
+  Fp2 u0, u1;
+  hash_to_field_fp2(msg, len, u0, u1);
+  G2J q0, q1;
+  map_to_curve_g2_pair(u0, u1, q0, q1);
+  (void)jac_add(q0, q1);
+}
+// k_hash_clear_x1 / _x2 / _fin on the message's mapped point
+static G2J g_hq, g_ht1, g_hu;
+void hc_k_hash_clear_setup(const uint8_t* msg, uint32_t len) {
+  Fp2 u0, u1;
+  hash_to_field_fp2(msg, len, u0, u1);
+  G2J q0, q1;
+  map_to_curve_g2_pair(u0, u1, q0, q1);
+  g_hq = jac_add(q0, q1);
+}
+void hc_k_hash_clear_x1(void) {
+  g_ht1 = jac_neg(jac_mul_xabs_in2(g_hq));
+  g_hu = jac_add_in<Fp2, true>(g_ht1, g2_psi(g_hq));
+}
+void hc_k_hash_clear_x2(void) { g_hu = jac_neg(jac_mul_xabs_in2(g_hu)); }
+void hc_k_hash_clear_fin(void) {
+  G2J t3 = g2_psi(g2_psi(jac_dbl_in(g_hq)));
+  t3 = jac_add_in<Fp2, true>(t3, jac_neg(g2_psi(g_hq)));
+  t3 = jac_add_in<Fp2, true>(t3, g_hu);
+  t3 = jac_add_in<Fp2, true>(t3, jac_neg(g_ht1));
+  (void)jac_add_in<Fp2, true>(t3, jac_neg(g_hq));
+}
+// k_hash_affine: one G2 to-affine conversion
+void hc_k_g2_affine(void) {
+  G2A a;
+  (void)jac_to_aff(jac_dbl(jac_from_aff(g_sig)), a);
+}
+// k_rlc_g1_l0: [r] pk from the key's pair table (the bucket additions are k_msm_bucket_part's)
+void hc_k_rlc_g1_l0(uint64_t r64) {
+  G1A ap, am;
+  rlc_pair_from_inv(g_pk, g_xpk, fp_inv(fp_reduce(fp_sub(g_xpk.x, g_pk.x))), ap, am);  // at key load
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  uint32_t u[4];
+  rlc_digits(r64, u);
+  (void)rlc_mul_table(ap, am, fp_from_const(G1_BETA), u);
+}
+// k_msm_bucket_part: one bucket entry (psi^k of a signature, one mixed addition)
+void hc_k_msm_entry(uint32_t k) {
+  G2J acc = jac_dbl(jac_from_aff(g_sig));
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  G2A p = msm_psi_k(g_sig, k);
+  (void)jac_add_aff_in(acc, p);
+}
+}  // extern "C"
+
+#include "../../charon_amd/csrc/bls_batchinv.h"
+// Montgomery's trick over workgroups (bls_batchinv.h, the device kernels'
+// batched to-affine / SSWU inversions), emulated lane by lane: n canonical
+// 48-byte big-endian values, present[i] = 0 marks an absent value (it takes
+// part as 1 and gets 1 back).  Also the work-model probes of its cost.
+extern "C" {
+void hc_batch_inv(const uint8_t* in48, const uint8_t* present, int n, int waves, uint8_t* out48) {
+  static Fp z[4096], r[4096];
+  static bool pr[4096];
+  if (n > 4096 || waves < 1 || waves > 16) return;
+  for (int i = 0; i < n; ++i) {
+    bool lt;
+    z[i] = fp_to_mont(fp_limbs_from_be48(in48 + 48 * i, &lt));
+    pr[i] = present[i] != 0;
+  }
+  batch_inv_emulate(z, pr, r, n, waves);
+  for (int i = 0; i < n; ++i) fp_limbs_to_be48(fp_from_mont(r[i]), out48 + 48 * i);
+}
+// u32 mul-adds of one fp_inv, and of the batched trick over n values
+void hc_fp_inv_once(void) {
+  Fp a = fp_from_const(ONE_M);
+  a = fp_add(a, a);
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  (void)fp_inv(a);
+}
+void hc_batch_inv_cost(int n, int waves) {
+  static Fp z[4096], r[4096];
+  static bool pr[4096];
+  Fp a = fp_from_const(ONE_M);
+  for (int i = 0; i < n && i < 4096; ++i) {
+    a = fp_add(a, fp_from_const(ONE_M));
+    z[i] = fp_reduce(a);
+    pr[i] = true;
+  }
+#if defined(TBG_COUNT_OPS)
+  tbg_mad_count = 0;
+#endif
+  batch_inv_emulate(z, pr, r, n, waves);
+}
+}  // extern "C"

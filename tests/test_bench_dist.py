@@ -51,24 +51,38 @@ def test_two_rank_max_over_ranks():
 
 
 def test_roofline_fields_from_work_model():
-    """bench.py's roofline arithmetic (no GPU): the pipelined chain's
-    achieved rate is units/s x algorithmic mul-adds per unit; the isolated
-    stage's is its mul-adds per launch / its launch time."""
-    import argparse
+    """bench.py's roofline arithmetic (no GPU): the dominant kernel by
+    exclusive time is priced with its own per-item work model x the launch's
+    items over its measured duration; the pipeline form is units/s x the
+    algorithmic mul-adds per unit."""
+    import types
+    import numpy as np
     import bench
     wm = bench.work_model()
-    assert wm is not None
-    args = argparse.Namespace(dvs=10000, t=3, n=4, merge=16)
-    iso = {"decode": 22.8, "hash": 16.6, "combine": 28.4, "h_lines": 6.5, "verify": 41.2, "aggregate": 2.8}
-    timed = {k: 3 * 1.5 * v for k, v in iso.items()}  # 3 launches of 16 batches, 1.5x slower when shared
-    stage, iso_r, pipe = bench.stage_rooflines(wm, iso, timed, args, 1.0e6, 48)
-    assert stage["kernel"].startswith("verify stage") and iso_r["kernel"].startswith("verify stage")
-    # timed-region form: work of the 48 steps over the summed launch time
-    assert abs(stage["achieved"] - stage["algorithmic_mads_per_launch"] * 3 / (timed["verify"] * 1e-3) / 1e12) < 1e-2
-    assert abs(iso_r["achieved"] - iso_r["algorithmic_mads_per_launch"] / 41.2e-3 / 1e12) < 1e-2
-    assert abs(iso_r["achieved"] / stage["achieved"] - 1.5) < 1e-3
-    assert abs(pipe["achieved"] - 1.0e6 * wm["mads"]["unit_3of4_rlc"] / 1e12) < 1e-2
+    assert wm is not None and "kernels" in wm
+    b = types.SimpleNamespace(n_dv=10000, identifiers=np.zeros(40000), msg_off=np.zeros(10001))
+    items = bench.launch_items([b] * 16, 16)
+    assert items == {"partial": 640000, "message": 160000, "duty": 160000, "group": 10000, "launch": 1}
+    prof = [("k_decode_sigs", 9.0), ("k_subgroup_sigs", 13.4), ("k_rlc_miller_chunks<MILLER_L0>", 15.9),
+            ("k_rlc_miller_chunks<MILLER_GROUP_S>", 0.005), ("k_msm_sum", 0.4), ("k_msm_sum", 0.1)]
+    kp = bench.kernel_profile(prof)
+    assert kp["k_msm_sum"] == (0.5, 2)
+    r = bench.kernel_roofline(wm, kp, items, None, 16)
+    m = wm["kernels"]["k_rlc_miller_chunks<MILLER_L0>"]
+    mads = m["mads"] * 10000 + m["plus_per_launch"]
+    assert r["kernel"] == "k_rlc_miller_chunks<MILLER_L0>" == r["dominant_by_exclusive_time"]
+    assert r["rocprof_name"] == "void tbg::k_rlc_miller_chunks<1>(tbg::DevBatch)"
+    assert r["algorithmic_mads_per_launch"] == mads
+    assert abs(r["achieved"] - mads / 15.9e-3 / 1e12) < 1e-2
+    assert abs(r["frac"] - r["achieved"] / bench.PEAK_MAD_TOPS) < 1e-3
+    # an unpriced dominant kernel falls to the longest priced one, and says so
+    kp2 = dict(kp, k_mystery=(99.0, 1))
+    r2 = bench.kernel_roofline(wm, kp2, items, None, 16)
+    assert r2["dominant_by_exclusive_time"] == "k_mystery" and r2["kernel"] == "k_rlc_miller_chunks<MILLER_L0>"
+    pipe = bench.pipeline_roofline(wm, 1.0e6, True, 3, 4)
+    assert abs(pipe["achieved"] - 1.0e6 * wm["mads"]["unit_3of4_l0"] / 1e12) < 1e-2
     assert 0 < pipe["frac"] < 1
+    assert bench.pipeline_roofline(wm, 1.0e6, True, 7, 10) is None
 
 
 def test_batch_exact_follows_injection():

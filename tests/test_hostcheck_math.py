@@ -398,3 +398,26 @@ def test_word_sha_expand_message_matches_byte_stream():
     for n in list(range(0, 20)) + [31, 32, 33, 63, 64, 65, 71, 72, 73, 127, 128, 136, 200, 255, 300]:
         msg = bytes((7 * k + n) & 0xFF for k in range(n))
         assert L.hc_h2f_check(msg, n) == 1, n
+
+
+def test_workgroup_batch_inversion_matches_per_value_inverse():
+    """bls_batchinv.h (Montgomery's trick over a workgroup: wave scans, one
+    inversion, back-substitution), emulated lane by lane: every present value
+    gets its own inverse, absent ones (a zero among them, the point at
+    infinity's Z) get 1 and do not disturb their neighbours; blocks of 1 and 4
+    waves, a partial last workgroup."""
+    import ctypes
+    for waves, n in ((4, 300), (1, 64), (4, 256), (2, 129)):
+        vals = [rng.randrange(1, P) for _ in range(n)]
+        present = [1] * n
+        for k in (0, 63, 64, 200, n - 1):
+            if k < n:
+                present[k] = 0
+        vals[min(5, n - 1)] = 0
+        present[min(5, n - 1)] = 0  # a zero element, marked absent as the kernels do
+        vals[min(7, n - 1)] = 1
+        out = ctypes.create_string_buffer(48 * n)
+        lib().hc_batch_inv(b"".join(be(v) for v in vals), bytes(present), n, waves, out)
+        got = [fe(out.raw[48 * i:48 * i + 48]) for i in range(n)]
+        for v, pz, g in zip(vals, present, got):
+            assert g == (pow(v, P - 2, P) if pz else 1)

@@ -91,6 +91,43 @@ def main():
     qmul = measure(lib.hc_stage_group_final, 2)[0] - final1
     s_quad, _ = measure(lib.hc_stage_miller_chunk, 0, 1)
     nch = G // C
+    # per-kernel probes (one item of each kernel of the level-0 chain)
+    for fn in ("hc_k_decode_sigs", "hc_k_subgroup_sigs"):
+        getattr(lib, fn).restype = ctypes.c_int
+    for fn in ("hc_k_hash_map", "hc_k_hash_clear_setup", "hc_k_hash_clear_x1", "hc_k_hash_clear_x2",
+               "hc_k_hash_clear_fin", "hc_k_g2_affine", "hc_k_rlc_g1_l0", "hc_k_msm_entry"):
+        getattr(lib, fn).restype = None
+    lib.hc_k_rlc_g1_l0.argtypes = [ctypes.c_uint64]
+    lib.hc_k_msm_entry.argtypes = [ctypes.c_uint32]
+    k_decode, st = measure(lib.hc_k_decode_sigs, sigs[0])
+    assert st == 0
+    k_subgroup, st = measure(lib.hc_k_subgroup_sigs, sigs[0])
+    assert st == 1
+    k_hash_map, _ = measure(lib.hc_k_hash_map, msg, len(msg))
+    lib.hc_k_hash_clear_setup(msg, len(msg))
+    k_clear_x1, _ = measure(lib.hc_k_hash_clear_x1)
+    k_clear_x2, _ = measure(lib.hc_k_hash_clear_x2)
+    k_clear_fin, _ = measure(lib.hc_k_hash_clear_fin)
+    k_g2_aff, _ = measure(lib.hc_k_g2_affine)
+    k_g1_l0, _ = measure(lib.hc_k_rlc_g1_l0, 0x9E3779B97F4A7C15)
+    k_msm_entry = sum(measure(lib.hc_k_msm_entry, k)[0] for k in range(4)) / 4
+    # Montgomery's trick over a workgroup (bls_batchinv.h): its per-value cost
+    # replaces one fp_inv in every batched kernel (k_hash_map's SSWU
+    # denominator, k_hash_affine, k_rlc_duty_sum, k_aggregate)
+    for fn in ("hc_fp_inv_once", "hc_batch_inv_cost"):
+        getattr(lib, fn).restype = None
+    lib.hc_batch_inv_cost.argtypes = [ctypes.c_int, ctypes.c_int]
+    fp_inv_cost, _ = measure(lib.hc_fp_inv_once)
+    binv_n = 256 * 8
+    binv_item = measure(lib.hc_batch_inv_cost, binv_n, 4)[0] / binv_n
+    saved = fp_inv_cost - binv_item  # per batched inversion
+    k_hash_map -= saved
+    k_g2_aff -= saved
+    agg -= saved
+    duty_sum_p4 -= saved
+    duty_sum4 -= saved
+    rlc_partial -= saved  # (k_rlc_partial2: the n2 inversion batched; its G1 product now from the key's table)
+    hash_ -= 2 * saved
     l0_per_group = nch * chunk2 + nch * qmul
     l0_per_launch = bucket_scales + (32768 + 2048 + 128 + 8) * g2_add + lines_h + s_quad + final1
     launch_dvs = 16 * 10000  # bench default: 16 batches of 10k DVs per launch
@@ -128,6 +165,27 @@ def main():
                           "unit_3of4_l0": unit_3of4_l0, "unit_3of4_rlc": unit_3of4_rlc,
                           "unit_3of4_each": unit_3of4, "unit_3of4_reference_schedule": unit_3of4_v1}.items()},
         "verify_hbm_bytes_per_launch": None,
+        "batched_inversion": {"fp_inv": fp_inv_cost, "per_value_in_workgroups_of_256": round(binv_item, 1)},
+        # u32 mul-adds per item of each kernel of the level-0 chain (bench.py
+        # prices the dominant kernel of its per-kernel profile with these)
+        "kernels": {
+            "k_decode_sigs": {"per": "partial", "mads": round(k_decode)},
+            "k_subgroup_sigs": {"per": "partial", "mads": round(k_subgroup)},
+            "k_hash_map": {"per": "message", "mads": round(k_hash_map)},
+            "k_hash_clear_x1": {"per": "message", "mads": round(k_clear_x1)},
+            "k_hash_clear_x2": {"per": "message", "mads": round(k_clear_x2)},
+            "k_hash_clear_fin": {"per": "message", "mads": round(k_clear_fin)},
+            "k_hash_affine": {"per": "message", "mads": round(k_g2_aff)},
+            "k_lines_h": {"per": "message", "mads": round(lines_h)},
+            "k_rlc_g1_l0": {"per": "partial", "mads": round(k_g1_l0)},
+            "k_msm_bucket_part": {"per": "partial", "mads": round(4 * k_msm_entry)},
+            "k_msm_bucket": {"per": "launch", "mads": round(bucket_scales + 32768 * (4 - 1) * g2_add)},
+            "k_rlc_duty_sum<DSUM_L0_P>": {"per": "duty", "mads": round(duty_sum_p4)},
+            "k_rlc_miller_chunks<MILLER_L0>": {"per": "group", "mads": round(nch * chunk2), "plus_per_launch": s_quad},
+            "k_l0_fold": {"per": "group", "mads": round((nch - 1) * qmul)},
+            "k_l0_final": {"per": "launch", "mads": round(final1)},
+            "k_aggregate": {"per": "duty", "mads": round(agg)},
+        },
     }
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "work_model.json"), "w") as f:
