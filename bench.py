@@ -117,8 +117,8 @@ STAGE_KERNELS = {
     "decode": ["k_decode_sigs", "k_subgroup_sigs"],
     "hash": ["k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
     "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_bucket_part", "k_msm_sum", "k_msm_scan", "k_msm_scatter",
-                "k_rlc_duty_sum", "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines",
-                "k_lines_fold<FOLD_GROUPS>"],
+                "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
+                "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>"],
     "h_lines": ["k_lines_h"],
     "verify": ["k_rlc_miller_chunks<MILLER_L0>", "k_rlc_miller_chunks<MILLER_GROUP_S>",
                "k_rlc_miller_chunks<MILLER_GROUPS>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after",
@@ -126,7 +126,10 @@ STAGE_KERNELS = {
                "k_rlc_check_chunks", "k_rlc_cident_lines", "k_lines_fold<FOLD_CID>", "k_rlc_cident_check",
                "k_rlc_ident_lines", "k_lines_fold<FOLD_IDENT>", "k_rlc_ident_check", "k_lines_sig_list",
                "k_verify_list"],
-    "aggregate": ["k_lagrange", "k_aggregate", "k_aggregate_finish"],
+    # (the speculative pass <true> runs mid-chain while level 0 is on; the
+    # regular pass <false> then returns at once after a level-0 pass)
+    "aggregate": ["k_lagrange<true>", "k_aggregate<true>", "k_aggregate_finish<true>", "k_lagrange<false>",
+                  "k_aggregate<false>", "k_aggregate_finish<false>"],
 }
 # profile name (launch site) -> the symbol rocprofv3 prints for it
 ROCPROF_NAME = {

@@ -6,18 +6,29 @@
 
 namespace tbg {
 
+// The speculative pass (SPEC) and the regular pass after it: see
+// participates<SPEC> (tbls_launch.h).  spec_done: a level-0 pass confirmed
+// the speculative results (the regular pass leaves them).
+__device__ __forceinline__ bool spec_skip(const DevBatch& B, bool spec) {
+  if (spec) return B.counters[CNT_L0_BAD] != 0;  // level 0 cannot pass: no speculation
+  return B.rlc_batch && B.op == TBG_OP_VERIFY_AGGREGATE && B.counters[CNT_L0_OK] != 0;
+}
+
+template <bool SPEC>
 __global__ void TBG_LAUNCH k_lagrange(DevBatch B) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (spec_skip(B, SPEC)) return;
+  if (i == 0) B.counters[CNT_AGG] = 0;  // (k_aggregate appends after this grid)
   if (i >= B.n_partials) return;
   uint32_t* w = B.lam + 8ull * i;
   for (int j = 0; j < 8; ++j) w[j] = 0;
-  if (!participates(B.op, B.partial_status[i])) return;
+  if (!participates<SPEC>(B.op, B.partial_status[i])) return;
   uint32_t d = B.partial_duty[i];
   uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
   uint8_t ids[256];
   int k = 0, me = -1;
   for (uint32_t j = first; j < last; ++j) {
-    if (!participates(B.op, B.partial_status[j])) continue;
+    if (!participates<SPEC>(B.op, B.partial_status[j])) continue;
     if (j == i) me = k;
     ids[k++] = B.identifiers[j];
   }
@@ -44,6 +55,7 @@ __device__ void agg_emit(const DevBatch& B, uint32_t d, const G2J& acc) {
 // listed here instead and finished by k_aggregate_finish in uniform waves.
 // The affine conversion of the finished sums is batched over the workgroup
 // (bls_batchinv.h): every thread reaches it, with or without a sum to emit.
+template <bool SPEC>
 __device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& emit) {
   emit = false;
   uint8_t* out = B.agg + 96ull * d;
@@ -55,7 +67,7 @@ __device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& em
   bool decode_err = false, identity = false;
   for (uint32_t j = first; j < last; ++j) {
     int32_t st = B.partial_status[j];
-    if (participates(B.op, st)) ++k;
+    if (participates<SPEC>(B.op, st)) ++k;
     if (st == TBG_PS_ERR_IDENTITY) identity = true;
     else if (st < 0 && st != TBG_PS_ERR_PUBKEY) decode_err = true;
   }
@@ -70,14 +82,14 @@ __device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& em
   if (k < 2) return TBG_DS_AGG_TOO_FEW;
   // duplicate identifiers among participants
   for (uint32_t a = first; a < last; ++a) {
-    if (!participates(B.op, B.partial_status[a])) continue;
+    if (!participates<SPEC>(B.op, B.partial_status[a])) continue;
     for (uint32_t b = a + 1; b < last; ++b) {
-      if (participates(B.op, B.partial_status[b]) && B.identifiers[a] == B.identifiers[b])
+      if (participates<SPEC>(B.op, B.partial_status[b]) && B.identifiers[a] == B.identifiers[b])
         return TBG_DS_AGG_DUPLICATE_ID;
     }
   }
   uint8_t mask[256];
-  for (uint32_t j = first; j < last; ++j) mask[j - first] = participates(B.op, B.partial_status[j]) ? 1 : 0;
+  for (uint32_t j = first; j < last; ++j) mask[j - first] = participates<SPEC>(B.op, B.partial_status[j]) ? 1 : 0;
   uint64_t D = 1;
   acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
   if (D > 1) {
@@ -89,12 +101,14 @@ __device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& em
   return TBG_DS_OK;
 }
 
+template <bool SPEC>
 __global__ void __launch_bounds__(BINV_BLOCK) k_aggregate(DevBatch B) {
+  if (spec_skip(B, SPEC)) return;  // (grid-uniform)
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = d < B.n_duties;
   G2J acc = jac_inf<Fp2>();
   bool emit = false;
-  int32_t st = in ? agg_prepare(B, d, acc, emit) : TBG_DS_OK;
+  int32_t st = in ? agg_prepare<SPEC>(B, d, acc, emit) : TBG_DS_OK;
   G2A a;
   const bool aff = block_jac_to_aff<BINV_WAVES>(acc, emit, a);  // every thread of the workgroup
   if (!in) return;
@@ -124,15 +138,17 @@ __device__ __forceinline__ G2J shfl_xor_g2j(const G2J& a, int m) {
 
 // [1/D] acc as the 4-way base-|x| MSM of bls_tss.h, one term per lane of a
 // quad (64 doublings each instead of 255 on one lane), summed over the quad.
+template <bool SPEC>
 __global__ void TBG_LAUNCH k_aggregate_finish(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t k = t >> 2;
   const int q = (int)(t & 3);
+  if (spec_skip(B, SPEC)) return;
   if (k >= B.counters[CNT_AGG]) return;  // quad-uniform
   const uint32_t d = B.agg_list[k];
   uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
   uint32_t j = first;
-  while (j < last && !participates(B.op, B.partial_status[j])) ++j;
+  while (j < last && !participates<SPEC>(B.op, B.partial_status[j])) ++j;
   const uint32_t* w = B.lam + 8ull * j;  // listed duties have a participant (k >= 2)
   uint64_t D = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
   uint64_t dg[4];
@@ -149,15 +165,21 @@ __global__ void TBG_LAUNCH k_aggregate_finish(DevBatch B) {
   if (q == 0) agg_emit(B, d, acc);
 }
 
-void launch_lagrange(const DevBatch& B, hipStream_t st) {
-  if (B.n_partials) TBG_KLAUNCH(k_lagrange, grid_for(B.n_partials), dim3(kBlock), st, B);
+void launch_lagrange(const DevBatch& B, hipStream_t st, bool spec) {
+  if (!B.n_partials) return;
+  if (spec) TBG_KLAUNCH(k_lagrange<true>, grid_for(B.n_partials), dim3(kBlock), st, B);
+  else TBG_KLAUNCH(k_lagrange<false>, grid_for(B.n_partials), dim3(kBlock), st, B);
 }
-void launch_aggregate(const DevBatch& B, hipStream_t st) {
-  if (B.n_duties)
-    TBG_KLAUNCH(k_aggregate, dim3((B.n_duties + BINV_BLOCK - 1) / BINV_BLOCK), dim3(BINV_BLOCK), st, B);
+void launch_aggregate(const DevBatch& B, hipStream_t st, bool spec) {
+  if (!B.n_duties) return;
+  const dim3 grid((B.n_duties + BINV_BLOCK - 1) / BINV_BLOCK);
+  if (spec) TBG_KLAUNCH(k_aggregate<true>, grid, dim3(BINV_BLOCK), st, B);
+  else TBG_KLAUNCH(k_aggregate<false>, grid, dim3(BINV_BLOCK), st, B);
 }
-void launch_aggregate_finish(const DevBatch& B, hipStream_t st) {
-  if (B.n_duties) TBG_KLAUNCH(k_aggregate_finish, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
+void launch_aggregate_finish(const DevBatch& B, hipStream_t st, bool spec) {
+  if (!B.n_duties) return;
+  if (spec) TBG_KLAUNCH(k_aggregate_finish<true>, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
+  else TBG_KLAUNCH(k_aggregate_finish<false>, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

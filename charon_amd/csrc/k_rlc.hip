@@ -36,6 +36,7 @@
 #include "bls_quad.h"
 #include "bls_rlc.h"
 #include "bls_batchinv.h"
+#include "bls_wide.h"
 
 namespace tbg {
 
@@ -310,15 +311,34 @@ __global__ void TBG_LAUNCH k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32
   quad_store(B.grp_f + (size_t)3 * QUAD_WORDS * (out + q), f);
 }
 
-// One quad: the last <= L0_TREE_FAN values times the S pair's product, one
-// final exponentiation for the whole batch.
-__global__ void TBG_LAUNCH k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
-  if (fp12_slot(threadIdx.x) != 0 || B.counters[CNT_L0_BAD]) return;
-  Fp4 f = quad_load(B.batch_f);
-  for (uint32_t a = 0; a < n; ++a) f = quad_mul(f, quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
-  f = quad_final_exp_in(quad_conj(f));
-  const bool ok = quad_is_one(f);
-  if (ok && threadIdx.x == 0) B.counters[CNT_L0_OK] = 1;
+// ONE wave: the last <= L0_TREE_FAN values times the S pair's product, one
+// final exponentiation for the whole batch -- the latency tail of every
+// level-0 launch, so the value is spread over the wave's lanes (bls_wide.h:
+// one Fp product per lane per step) instead of one trio.
+struct WideDevExec {
+  template <class Fn>
+  __device__ void operator()(Fn&& fn) {
+    fn((int)threadIdx.x);
+    __syncthreads();
+  }
+};
+__global__ void __launch_bounds__(64) k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
+  if (B.counters[CNT_L0_BAD]) return;  // (workgroup-uniform)
+  __shared__ WideSlots S;
+  WideDevExec ex;
+  const int l = threadIdx.x;
+  // quad layout in HBM: Fp v of A_q at (4 q + k) NL -- the wide order
+  auto load = [&](int slot, const uint32_t* src) {
+    if (l < WIDE_FP)
+      for (int j = 0; j < NL; ++j) S.v[slot][l].l[j] = src[l * NL + j];
+  };
+  ex([&](int) { load(0, B.batch_f); });
+  for (uint32_t a = 0; a < n; ++a) {
+    ex([&](int) { load(1, B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)); });
+    wide_mul_to(ex, S, 0, 0, 1);
+  }
+  wide_final_exp(ex, S);
+  if (l == 0 && wide_is_one(S.v[0])) B.counters[CNT_L0_OK] = 1;
 }
 
 // One thread per group: after a level-0 pass every group with a combined

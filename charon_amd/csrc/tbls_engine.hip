@@ -367,6 +367,10 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
     return e ? atoi(e) : 0;
   }();
   const bool sig_first = alt_order && st2 == st && ((&sl - c->slots.data()) & 1);
+  // Level 0 on: aggregate speculatively (every candidate valid) in the
+  // middle of the chain, so the launch's tail is the verification alone; the
+  // regular aggregation below returns at once after a level-0 pass.
+  const bool spec = B.op == TBG_OP_VERIFY_AGGREGATE && B.rlc_batch && B.rlc_group;
   auto msg_chain = [&]() -> int {
     HIP_TRY(hipEventRecord(ev[3], st2));
     if (verify) launch_hash_msgs(B, st2);
@@ -382,6 +386,11 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
     if (verify)
       launch_rlc_prepare(B, pk, (const G1A*)c->d_xpk, (const G1A*)c->d_pktab, (const int32_t*)c->d_pk_status, c->n_pk,
                          st);
+    if (spec) {  // the aggregation a level-0 pass will confirm, before the verification tail
+      launch_lagrange(B, st, true);
+      launch_aggregate(B, st, true);
+      launch_aggregate_finish(B, st, true);
+    }
     HIP_TRY(hipEventRecord(ev[2], st));
     return TBG_OK;
   };

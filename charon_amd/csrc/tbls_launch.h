@@ -157,9 +157,14 @@ enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT
 TBG_HD bool fb_in_pass(const DevBatch& B, uint32_t k) { return B.fb_window == 0 || k - B.fb_base < B.fb_window; }
 TBG_HD size_t fb_slot(const DevBatch& B, uint32_t k) { return (size_t)LINES_WORDS * (k - B.fb_base); }
 
-// Participation of a partial in its duty's aggregate.
+// Participation of a partial in its duty's aggregate.  SPEC: the
+// speculative aggregation that runs BEFORE verification while level 0 is on
+// (launch_chain): every candidate counts as valid, which is what a level-0
+// pass concludes; after a failed level 0 the aggregation runs again.
+template <bool SPEC = false>
 TBG_HD bool participates(uint32_t op, int32_t st) {
-  return op == TBG_OP_VERIFY_AGGREGATE ? (st == TBG_PS_VALID) : (st == TBG_PS_NOT_VERIFIED);
+  return op == TBG_OP_VERIFY_AGGREGATE ? (st == TBG_PS_VALID || (SPEC && st == TBG_PS_NOT_VERIFIED))
+                                       : (st == TBG_PS_NOT_VERIFIED);
 }
 
 // Debug aid: with TBG_DEBUG_SYNC=1 in the environment every launch is
@@ -212,9 +217,12 @@ void launch_l0_check(const DevBatch& B, hipStream_t st);
 // pk_tab: the keys' pair tables (k_pubkey_tables); unused after a level-0 failure (level 0 formed the G1 products)
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);
-void launch_lagrange(const DevBatch& B, hipStream_t st);
-void launch_aggregate(const DevBatch& B, hipStream_t st);
-void launch_aggregate_finish(const DevBatch& B, hipStream_t st);
+// spec: the speculative pass (level 0 on, before verification; skipped when
+// level 0 already cannot pass); the regular pass then returns at once if
+// level 0 passed
+void launch_lagrange(const DevBatch& B, hipStream_t st, bool spec = false);
+void launch_aggregate(const DevBatch& B, hipStream_t st, bool spec = false);
+void launch_aggregate_finish(const DevBatch& B, hipStream_t st, bool spec = false);
 void launch_sk_to_pk(const uint8_t* sk32, uint32_t n, uint8_t* pk48, hipStream_t st);
 void launch_sign(const uint8_t* sk32, const uint32_t* item_msg, uint32_t n, const G2A* h_aff, const int32_t* h_status,
                  uint8_t* sig96, hipStream_t st);

@@ -743,3 +743,28 @@ void hc_batch_inv_cost(int n, int waves) {
   batch_inv_emulate(z, pr, r, n, waves);
 }
 }  // extern "C"
+
+#include "../../charon_amd/csrc/bls_wide.h"
+// The wave-wide Fp12 of bls_wide.h (k_l0_final's final exponentiation),
+// lanes emulated phase by phase: FE of a, and a * b.
+extern "C" {
+static void wide_load(tbg::Fp* v, const Fp12& f) {
+  for (int q = 0; q < 3; ++q) wide_put4(v, q, quad_from_fp12(q, f));
+}
+static Fp12 wide_store(const tbg::Fp* v) { return quad_to_fp12(wide_fp4(v, 0), wide_fp4(v, 1), wide_fp4(v, 2)); }
+void hc_wide_final_exp(const uint8_t* a, uint8_t* out) {
+  static WideSlots S;
+  wide_load(S.v[0], f12_in(a));
+  WideHostExec ex;
+  wide_final_exp(ex, S);
+  f12_out(wide_store(S.v[0]), out);
+}
+void hc_wide_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  static WideSlots S;
+  wide_load(S.v[1], f12_in(a));
+  wide_load(S.v[2], f12_in(b));
+  WideHostExec ex;
+  wide_mul_to(ex, S, 0, 1, 2);
+  f12_out(wide_store(S.v[0]), out);
+}
+}

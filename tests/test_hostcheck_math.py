@@ -421,3 +421,12 @@ def test_workgroup_batch_inversion_matches_per_value_inverse():
         got = [fe(out.raw[48 * i:48 * i + 48]) for i in range(n)]
         for v, pz, g in zip(vals, present, got):
             assert g == (pow(v, P - 2, P) if pz else 1)
+
+
+def test_wide_fp12_final_exp_matches_oracle():
+    """bls_wide.h (one Fp12 over a wave's lanes, k_l0_final): the product and
+    the whole final exponentiation, lanes emulated phase by phase, equal the
+    oracle's; a Miller value that passes its check exponentiates to 1."""
+    a, b = rand_f12(), rand_f12()
+    assert b2f12(call("hc_wide_mul", f12b(a), f12b(b), out=576)) == bls.f12_mul(a, b)
+    assert b2f12(call("hc_wide_final_exp", f12b(a), out=576)) == bls.final_exp(a)

@@ -184,7 +184,8 @@ def main():
             "k_rlc_miller_chunks<MILLER_L0>": {"per": "group", "mads": round(nch * chunk2), "plus_per_launch": s_quad},
             "k_l0_fold": {"per": "group", "mads": round((nch - 1) * qmul)},
             "k_l0_final": {"per": "launch", "mads": round(final1)},
-            "k_aggregate": {"per": "duty", "mads": round(agg)},
+            "k_aggregate<true>": {"per": "duty", "mads": round(agg)},
+            "k_aggregate<false>": {"per": "duty", "mads": round(agg)},
         },
     }
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
