@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <new>
 #include <random>
@@ -352,7 +353,12 @@ ready:
 // Events: ev[0] start, ev[1] decode done, ev[2] combine done, ev[3]/ev[4]
 // hash start/done and ev[5] H lines done (st2), ev[6] verify start, ev[7]
 // verify done, ev[8] lagrange done, ev[9] aggregate done, ev[10] decode start.
-static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_t* ev) {
+// `stage` enqueues one part (0: start + the first chain, 1: the second
+// chain, 2: the checks and the aggregation; -1: all three): a replay of
+// several slots enqueues stage 0 of every slot before stage 1 of any, so the
+// slots' first kernels start together instead of one chain's enqueue time
+// (~100 launches) apart.
+static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_t* ev, int stage = -1) {
   hipStream_t st = sl.st, st2 = sl.st2;
   const bool verify = B.op != TBG_OP_AGGREGATE;
   const G1A* pk = (const G1A*)c->d_pk;
@@ -394,14 +400,15 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
     HIP_TRY(hipEventRecord(ev[2], st));
     return TBG_OK;
   };
-  HIP_TRY(hipEventRecord(ev[0], st));
-  HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
   int rc;
-  if (sig_first) {
-    if ((rc = sig_chain()) != TBG_OK || (rc = msg_chain()) != TBG_OK) return rc;
-  } else {
-    if ((rc = msg_chain()) != TBG_OK || (rc = sig_chain()) != TBG_OK) return rc;
+  if (stage < 0 || stage == 0) {
+    HIP_TRY(hipEventRecord(ev[0], st));
+    HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
+    if ((rc = sig_first ? sig_chain() : msg_chain()) != TBG_OK) return rc;
   }
+  if (stage < 0 || stage == 1)
+    if ((rc = sig_first ? msg_chain() : sig_chain()) != TBG_OK) return rc;
+  if (stage >= 0 && stage != 2) return TBG_OK;
   HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
   HIP_TRY(hipEventRecord(ev[6], st));
   if (verify) launch_rlc_check(B, pk, (const G1A*)c->d_xpk, (const int32_t*)c->d_pk_status, c->n_pk, st);
@@ -880,9 +887,17 @@ int tbg_replay_plan(tbg_ctx* c, const tbg_ticket* tickets, const uint32_t* n_par
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   int rc = TBG_OK;
   // Launch k on the streams of its slot: launches of different slots are in
-  // flight together, launches of one slot run in order.
-  for (uint32_t k = 0; k < n_launches && rc == TBG_OK; ++k)
-    rc = launch_chain(c, *sl[k], bs[k], ev.data() + (size_t)kChainEvents * k);
+  // flight together, launches of one slot run in order.  Runs of launches on
+  // distinct slots are enqueued stage by stage (launch_chain), so their
+  // first kernels start together.
+  for (uint32_t k0 = 0; k0 < n_launches && rc == TBG_OK;) {
+    uint32_t k1 = k0 + 1;
+    while (k1 < n_launches && std::find(sl.begin() + k0, sl.begin() + k1, sl[k1]) == sl.begin() + k1) ++k1;
+    for (int stage = 0; stage < 3 && rc == TBG_OK; ++stage)
+      for (uint32_t k = k0; k < k1 && rc == TBG_OK; ++k)
+        rc = launch_chain(c, *sl[k], bs[k], ev.data() + (size_t)kChainEvents * k, stage);
+    k0 = k1;
+  }
   for (uint32_t k = 0; k < n_launches; ++k) {
     if (hipStreamSynchronize(sl[k]->st) != hipSuccess) rc = TBG_E_DEVICE;
     if (hipStreamSynchronize(sl[k]->st2) != hipSuccess) rc = TBG_E_DEVICE;
