@@ -120,7 +120,7 @@ STAGE_KERNELS = {
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
                 "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>"],
     "h_lines": ["k_lines_h"],
-    "verify": ["k_rlc_miller_chunks<MILLER_L0>", "k_rlc_miller_chunks<MILLER_GROUP_S>",
+    "verify": ["k_l0_miller_hex", "k_rlc_miller_chunks<MILLER_L0>", "k_rlc_miller_chunks<MILLER_GROUP_S>",
                "k_rlc_miller_chunks<MILLER_GROUPS>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after",
                "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_chunk_lines", "k_lines_fold<FOLD_CHUNKS>",
                "k_rlc_check_chunks", "k_rlc_cident_lines", "k_lines_fold<FOLD_CID>", "k_rlc_cident_check",
@@ -133,6 +133,7 @@ STAGE_KERNELS = {
 }
 # profile name (launch site) -> the symbol rocprofv3 prints for it
 ROCPROF_NAME = {
+    "k_l0_miller_hex": "tbg::k_l0_miller_hex(tbg::DevBatch)",
     "k_rlc_miller_chunks<MILLER_L0>": "void tbg::k_rlc_miller_chunks<1>(tbg::DevBatch)",
     "k_rlc_miller_chunks<MILLER_GROUP_S>": "void tbg::k_rlc_miller_chunks<2>(tbg::DevBatch)",
     "k_rlc_miller_chunks<MILLER_GROUPS>": "void tbg::k_rlc_miller_chunks<0>(tbg::DevBatch)",

@@ -1,0 +1,236 @@
+// Hexad Fp12: one Fp12 per SIX lanes -- the trio of bls_quad.h with every Fp2
+// split over a lane pair (bls_pair.h), so the per-lane state halves.
+//
+// Why: the level-0 Miller-chunk kernel in the trio layout needs ~450 VGPRs
+// per lane (f = one Fp4 = 56 VGPRs, the Fp4 products and the streamed line
+// values on top), so it runs at ONE wave per SIMD, where gfx950 issues
+// v_mad_u64_u32 at ~58 % of the two-wave rate (profiles/r02/valu_rates.txt):
+// 0.49 of the VALU peak was its ceiling.  A hexad lane holds
+// one COMPONENT of its trio lane's Fp4 (a_c, b_c: 28 VGPRs) and computes
+// component c of every Fp2 product as one REDC(ab + cd) -- the same
+// multiply count per Fp12 as the trio (half per lane, twice the lanes) at
+// half the live state, so the kernel fits 256 VGPRs: two waves per SIMD.
+//
+// Layout: trio lane q = (lane & 15) % 3 as in bls_quad.h (5 trios per DPP
+// row, lane 15 idle) in BOTH halves of the wave; component c = lane >> 5
+// (lanes 0..31 hold c0, lanes 32..63 c1, partner = lane ^ 32, one
+// v_permlane32_swap per word).  Trio exchanges stay DPP row shifts on the
+// own component.  A wave carries 10 Fp12 values (60 of 64 lanes work).
+//
+// Cross-component terms (the multiplications by xi = 1 + u hidden in the
+// Fp4 / Fp12 algebra) need the partner's component of ONE value per
+// operation, so each product or squaring swaps its operand once (for the
+// pair products) and one intermediate (for the xi term).
+//
+// The per-lane pieces are plain functions of (c, q, own, partner, ...) so
+// the host build checks the algebra by emulating the six lanes
+// (tests/hostcheck: hc_hex_*), against the tower and the trio.
+#pragma once
+#include "bls_quad.h"
+#include "bls_pair.h"
+
+namespace tbg {
+
+struct Fp4h { Fp a, b; };  // component c of a trio lane's A_q = (a, b)
+// An Fp2 as lane c sees it: its own component o = x_c and its partner's p =
+// x_(1-c).  Products and linear maps work on this form directly, so no lane
+// ever selects components out of a whole Fp2 (per-limb selects cost as much
+// as a tenth of a product each).
+struct Fp2o { Fp o, p; };
+struct Fp4o { Fp2o a, b; };
+
+TBG_HD Fp4h hx_select(bool k, const Fp4h& x, const Fp4h& y) { return {fp_select(k, x.a, y.a), fp_select(k, x.b, y.b)}; }
+TBG_HD Fp2o hx_add(const Fp2o& x, const Fp2o& y) { return {fp_add(x.o, y.o), fp_add(x.p, y.p)}; }
+// xi x = (x0 - x1) + (x0 + x1) u seen from lane c (lazy: < x + 16p)
+TBG_HD Fp2o hx_mul_xi(uint32_t c, const Fp2o& x) {
+  const Fp s = fp_add(x.o, x.p), d0 = fp_sub(x.o, x.p), d1 = fp_sub(x.p, x.o);
+  return {fp_select(c != 0, s, d0), fp_select(c != 0, d1, s)};
+}
+// component c of x y (one REDC(ab + cd)); x < 32p, y's partner < 16p
+TBG_HD Fp hx_mul(uint32_t c, const Fp2o& x, const Fp2o& y) { return pair_mul_lane(c, x.o, x.p, y.o, y.p); }
+// component c of xi x from x's own / partner components (lazy: < x0 + 16p)
+TBG_HD Fp hx_xi(uint32_t c, const Fp& own, const Fp& par) { return pair_mul_xi_lane(c, own, par); }
+// host tests: lane c's view of a whole value
+TBG_HD Fp2o hx_view(uint32_t c, const Fp2& x) { return c ? Fp2o{x.c1, x.c0} : Fp2o{x.c0, x.c1}; }
+TBG_HD Fp4o hx_view4(uint32_t c, const Fp4& x) { return {hx_view(c, x.a), hx_view(c, x.b)}; }
+
+// ---- fp4_sqr(x) = {a^2 + xi b^2, 2ab} in two phases around one exchange
+// phase 1: component c of ab and s = (a + xi b)(a + b)
+// (the lazy a + xi b, up to 24p, as the left operand: pair_mul_lane negates
+// the right one's partner component, which must stay < 16p)
+TBG_HD void hx_sqr1(uint32_t c, const Fp4o& x, Fp& ab, Fp& s) {
+  ab = hx_mul(c, x.a, x.b);
+  s = hx_mul(c, hx_add(x.a, hx_mul_xi(c, x.b)), hx_add(x.a, x.b));
+}
+// phase 2 (ab's partner component abp): component c of {t0, reduce(t1)}
+TBG_HD Fp4h hx_sqr2(uint32_t c, const Fp& ab, const Fp& abp, const Fp& s) {
+  const Fp u = fp_reduce(fp_add(ab, hx_xi(c, ab, abp)));
+  return {fp_reduce(fp_sub(s, u)), fp_reduce(fp_add(ab, ab))};
+}
+
+// ---- quad_combine for component c.  Phase 1: T and V, the value whose xi
+// multiple enters C.a (T.b on lane 0, Pn.b on lane 1); phase 2 with V's
+// partner component.
+TBG_HD void hx_comb1(int q, const Fp4h& P, const Fp4h& Pn, const Fp4h& Pp, const Fp4h& Qx, Fp4h& T, Fp& V) {
+  const Fp4h f1 = hx_select(q == 1, Pp, Pn);
+  const Fp4h f2 = hx_select(q == 0, Pp, P);
+  T = {fp_reduce(fp_sub(Qx.a, fp_add(f1.a, f2.a))), fp_reduce(fp_sub(Qx.b, fp_add(f1.b, f2.b)))};
+  V = fp_select(q == 0, T.b, Pn.b);
+}
+TBG_HD Fp4h hx_comb2(uint32_t c, int q, const Fp4h& P, const Fp4h& Pn, const Fp4h& Pp, const Fp4h& T, const Fp& V,
+                     const Fp& Vp) {
+  const Fp xv = fp_reduce(hx_xi(c, V, Vp));
+  // q = 0: (xv + P.a, T.a + P.b); q = 1: (T.a + xv, T.b + Pn.a); q = 2: (T.a + Pp.a, T.b + Pp.b)
+  const Fp x0 = fp_select(q == 0, xv, T.a);
+  const Fp y0 = fp_select(q == 0, P.a, fp_select(q == 1, xv, Pp.a));
+  const Fp x1 = fp_select(q == 0, T.a, T.b);
+  const Fp y1 = fp_select(q == 0, P.b, fp_select(q == 1, Pn.a, Pp.b));
+  return {fp_reduce(fp_add(x0, y0)), fp_reduce(fp_add(x1, y1))};
+}
+
+// ---- f * line, line = L0 + L2 x^2 with L0 = (l0, l4), L2 = l1 (evaluated):
+//   C_q = A_q L0 + (q < 2 ? y : 1) A_{q+1} l1   (quad_line_lane)
+// phase 1: the five products' components and W, the value whose xi multiple
+// enters C.a (t1, plus u.b on lanes 0, 1)
+struct HxLine { Fp t0, t1, s, ua, ub, W; };
+TBG_HD void hx_line_u(uint32_t c, const Fp4o& An, const Fp2o& l1, HxLine& r) {
+  r.ua = hx_mul(c, An.a, l1);
+  r.ub = hx_mul(c, An.b, l1);
+}
+TBG_HD void hx_line_t(uint32_t c, int q, const Fp4o& A, const Fp2o& l0, const Fp2o& l4, HxLine& r) {
+  r.t0 = hx_mul(c, A.a, l0);
+  r.t1 = hx_mul(c, A.b, l4);
+  r.s = hx_mul(c, hx_add(A.a, A.b), hx_add(l0, l4));
+  r.W = fp_add(r.t1, fp_select(q < 2, r.ub, fp_zero()));
+}
+// phase 2 (W's partner component Wp)
+TBG_HD Fp4h hx_line2(uint32_t c, int q, const HxLine& r, const Fp& Wp) {
+  const Fp xw = hx_xi(c, r.W, Wp);                                 // < 20p
+  const Fp ca = fp_reduce(fp_add(fp_add(r.t0, xw), fp_select(q < 2, fp_zero(), r.ua)));
+  const Fp c1 = fp_sub(r.s, fp_add(r.t0, r.t1));                   // < 18p
+  return {ca, fp_reduce(fp_add(c1, fp_select(q < 2, r.ua, r.ub)))};
+}
+
+}  // namespace tbg
+
+// ---------------------------------------------------------------------------
+// Device: the hexad as lanes of a wave.
+#if defined(__HIP__)
+namespace tbg {
+
+// Fp12 slot of global thread t (UINT32_MAX for lane 15 of a row), and the
+// threads n slots need: 10 per wave.
+TBG_HD inline uint32_t hex_slot(uint32_t t) {
+  const uint32_t l = t & 15u;
+  return l == 15u ? 0xFFFFFFFFu : (t >> 6) * 10u + ((t >> 4) & 1u) * 5u + l / 3u;
+}
+inline uint32_t hex_threads(uint32_t n) { return 64u * ((n + 9u) / 10u); }
+TBG_DEV uint32_t hex_c() { return (threadIdx.x >> 5) & 1u; }
+
+// the partner lane's (lane ^ 32) value
+TBG_DEV uint32_t hx_swap_u32(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (threadIdx.x & 32u) ? r[0] : r[1];
+}
+TBG_DEV Fp hx_swap(const Fp& x) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = hx_swap_u32(x.l[i]);
+  return r;
+}
+TBG_DEV Fp4h hx_swap(const Fp4h& x) { return {hx_swap(x.a), hx_swap(x.b)}; }
+template <int K>
+TBG_DEV Fp4h hxch(const Fp4h& x) { return {xch<K>(x.a), xch<K>(x.b)}; }
+
+TBG_DEV Fp4h hex_one() {
+  Fp4h r = {fp_zero(), fp_zero()};
+  if (quad_lane() == 0 && hex_c() == 0) r.a = fp_one();
+  return r;
+}
+
+TBG_DEV Fp4o hx_own_par(const Fp4h& own, const Fp4h& par) { return {{own.a, par.a}, {own.b, par.b}}; }
+
+// f^2 (quad_sqr_in on the hexad)
+TBG_DEV Fp4h hex_sqr(const Fp4h& A) {
+  const uint32_t c = hex_c();
+  const int q = quad_lane();
+  Fp ab, s;
+  hx_sqr1(c, hx_own_par(A, hx_swap(A)), ab, s);
+  const Fp4h P = hx_sqr2(c, ab, hx_swap(ab), s);
+  const Fp4h SA = {fp_add(xch<QP_NEXT>(A.a), xch<QP_PREV>(A.a)), fp_add(xch<QP_NEXT>(A.b), xch<QP_PREV>(A.b))};
+  hx_sqr1(c, hx_own_par(SA, hx_swap(SA)), ab, s);
+  const Fp4h Q = hx_sqr2(c, ab, hx_swap(ab), s);
+  const Fp4h Pn = hxch<QP_NEXT>(P), Pp = hxch<QP_PREV>(P), Qx = hxch<QP_SW12>(Q);
+  Fp4h T;
+  Fp V;
+  hx_comb1(q, P, Pn, Pp, Qx, T, V);
+  return hx_comb2(c, q, P, Pn, Pp, T, V, hx_swap(V));
+}
+
+// f * (l0, l1, l4) in the order that keeps the live set small: the two
+// A_{q+1} l1 products first (A_{q+1}'s partner components by a swap of the
+// exchanged own ones), then A_q (l0, l4) with l0 loaded only then
+// (`l0_src`: the line's first 2 NL words, or null with l0 given)
+TBG_DEV Fp4h hex_line_mul(const Fp4h& A, const uint32_t* l0_src, Fp2o l0, const Fp2o& l1, const Fp2o& l4) {
+  const uint32_t c = hex_c();
+  const int q = quad_lane();
+  HxLine r;
+  {
+    const Fp4h An = hxch<QP_NEXT>(A);
+    hx_line_u(c, hx_own_par(An, hx_swap(An)), l1, r);
+  }
+  if (l0_src) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      l0.o.l[i] = l0_src[c * NL + i];
+      l0.p.l[i] = l0_src[(c ^ 1u) * NL + i];
+    }
+  }
+  hx_line_t(c, q, hx_own_par(A, hx_swap(A)), l0, l4, r);
+  return hx_line2(c, q, r, hx_swap(r.W));
+}
+
+// f *= line(idx) of stored (unevaluated) lines at affine P = (-x, y): lane
+// (0, c) evaluates l1_c (-x), lane (1, c) l4_c y; the trio broadcasts them
+// and the pair swaps the other components
+TBG_DEV Fp4h hex_line_at(const Fp4h& A, const uint32_t* lines, int idx, const Fp& nx, const Fp& y) {
+  const uint32_t c = hex_c();
+  const int q = quad_lane();
+  const uint32_t* src = lines + LINE_WORDS * idx;
+  Fp lk;
+  const int k = q == 0 ? 2 : 4;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) lk.l[i] = src[(k + (int)c) * NL + i];
+  const Fp e = fp_mul(lk, fp_select(q == 0, nx, y));
+  const Fp e1 = xch<QP_B0>(e), e4 = xch<QP_B1>(e);
+  return hex_line_mul(A, src, Fp2o{}, Fp2o{e1, hx_swap(e1)}, Fp2o{e4, hx_swap(e4)});
+}
+// f *= line(idx) of folded (already evaluated) lines
+TBG_DEV Fp4h hex_line_folded(const Fp4h& A, const uint32_t* lines, int idx) {
+  const uint32_t c = hex_c();
+  const uint32_t* src = lines + LINE_WORDS * idx;
+  Fp2o l[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      l[k].o.l[i] = src[(2 * k + (int)c) * NL + i];
+      l[k].p.l[i] = src[(2 * k + (int)(c ^ 1u)) * NL + i];
+    }
+  return hex_line_mul(A, nullptr, l[0], l[1], l[2]);
+}
+
+// quad layout in HBM (bls_quad.h / k_rlc.hip QUAD_WORDS = 4 NL per trio
+// lane, [a.c0, a.c1, b.c0, b.c1]): lane (q, c) writes its two components
+TBG_DEV void hex_store(uint32_t* dst, const Fp4h& A) {
+  const int q = quad_lane();
+  const uint32_t c = hex_c();
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    dst[4 * NL * q + c * NL + j] = A.a.l[j];
+    dst[4 * NL * q + (2 + c) * NL + j] = A.b.l[j];
+  }
+}
+
+}  // namespace tbg
+#endif

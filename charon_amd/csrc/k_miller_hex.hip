@@ -1,0 +1,78 @@
+// Level 0's P-chunk Miller products on hexads (bls_hex.h): the MILLER_L0 mode
+// of k_rlc_miller_chunks (k_rlc.hip) with each Fp12 spread over six lanes
+// instead of three, so the kernel fits 256 VGPRs and runs at two waves per
+// SIMD.  Same slots, same products, same quad-layout output (chunk_f,
+// batch_f): the level-0 fold / tree / final kernels and the group levels read
+// them unchanged.  Reference: the pairing products behind tbls.Verify
+// (tbls/tss.go:190-197), batched per k_rlc.hip's header.
+//
+// Products are kept in program order (TBG_SCHED_FENCE): interleaving two
+// independent Montgomery products for ILP is what pushes a kernel past 256
+// registers, and the second wave per SIMD hides the latency instead.
+#ifndef TBG_SCHED_FENCE
+#define TBG_SCHED_FENCE 1
+#endif
+#include "tbls_launch.h"
+#include "bls_lines.h"
+#include "bls_hex.h"
+
+namespace tbg {
+
+#ifndef TBG_HEX_WAVES
+#define TBG_HEX_WAVES 2
+#endif
+
+// One hexad per (group, chunk of rlc_chunk duties), then ONE hexad for level
+// 0's S pair (batch lines folded with -g1), as k_rlc_miller_chunks<MILLER_L0>.
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_l0_miller_hex(DevBatch B) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk;
+  const uint32_t n_groups = (B.n_duties + G - 1) / G;
+  const uint32_t nch = (G + C - 1) / C, nq = nch + 1;
+  const uint32_t np_q = n_groups * nch;
+  const uint32_t qd = hex_slot(t);
+  if (qd == 0xFFFFFFFFu || qd >= np_q + 1) return;
+  const bool s_quad = qd == np_q;
+  const uint32_t* ls;
+  uint32_t* dst;
+  uint32_t d0 = 0, d1 = 0;
+  if (s_quad) {
+    if (B.counters[CNT_L0_BAD]) return;
+    ls = B.batch_lines;
+    dst = B.batch_f;
+  } else {
+    const uint32_t g = qd / nch, c = qd % nch;
+    d0 = g * G + c * C;
+    d1 = min(d0 + C, min(g * G + G, B.n_duties));
+    ls = nullptr;
+    dst = B.chunk_f + (size_t)3 * 4 * NL * (g * nq + c);
+  }
+  Fp4h f = hex_one();
+  int idx = 0;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = hex_sqr(f);
+    const int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+#pragma unroll 1
+    for (int s = 0; s < steps; ++s, ++idx) {
+      if (s_quad) f = hex_line_folded(f, ls, idx);
+#pragma unroll 1
+      for (uint32_t d = d0; d < d1; ++d) {
+        if (B.dv_state[d] != RLC_COMBINED) continue;
+        const uint32_t m = B.duty_msg[d];
+        if (B.h_status[m] != 0) continue;  // level 0 fails in k_l0_fold
+        const G1A& P = B.dv_p[d];
+        f = hex_line_at(f, B.h_lines + (size_t)LINES_WORDS * m, idx, fp_reduce(fp_neg(P.x)), P.y);
+      }
+    }
+  }
+  hex_store(dst, f);
+}
+
+void launch_l0_miller_hex(const DevBatch& B, hipStream_t st) {
+  const uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
+  const uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
+  TBG_KLAUNCH(k_l0_miller_hex, grid_for(hex_threads(n_groups * nch + 1)), dim3(kBlock), st, B);
+}
+
+}  // namespace tbg

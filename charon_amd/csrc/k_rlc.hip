@@ -762,7 +762,15 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
     if (B.rlc_batch) {
       // level 0: the P chunks (kept for the group levels) and S, one product
-      TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_L0>, grid_for(fp12_threads((n_groups * nch + 1))), dim3(kBlock), st, B);
+      // (on hexads by default: two waves per SIMD; TBG_L0_HEX=0 runs the trio form)
+      static const bool hex = [] {
+        const char* e = getenv("TBG_L0_HEX");
+        return !e || atoi(e) != 0;
+      }();
+      if (hex)
+        launch_l0_miller_hex(B, st);
+      else
+        TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_L0>, grid_for(fp12_threads((n_groups * nch + 1))), dim3(kBlock), st, B);
       TBG_KLAUNCH(k_l0_fold, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
       uint32_t in = 0, n = n_groups, out = n_groups;
       while (n > L0_TREE_FAN) {

@@ -214,6 +214,8 @@ void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStr
 void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab, hipStream_t st);
 void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
 void launch_l0_check(const DevBatch& B, hipStream_t st);
+// level 0's P-chunk and S Miller products on hexads (k_miller_hex.hip)
+void launch_l0_miller_hex(const DevBatch& B, hipStream_t st);
 // pk_tab: the keys' pair tables (k_pubkey_tables); unused after a level-0 failure (level 0 formed the G1 products)
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);

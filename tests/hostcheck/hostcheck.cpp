@@ -230,6 +230,55 @@ void hc_quad_conj(const uint8_t* a, uint8_t* out) {
 }
 }
 
+#include "../../charon_amd/csrc/bls_hex.h"
+// Host emulation of the hexad (bls_hex.h): trio lane q and component c run
+// in turn, the pair swap and the DPP exchanges become array indexing.
+extern "C" {
+static void hx_split(const Fp12& f, Fp4 (&A)[3]) { q_split(f, A); }
+static Fp12 hx_join(const Fp4h (&R)[3][2]) {
+  Fp4 C[3];
+  for (int q = 0; q < 3; ++q) C[q] = {{R[q][0].a, R[q][1].a}, {R[q][0].b, R[q][1].b}};
+  return quad_to_fp12(C[0], C[1], C[2]);
+}
+void hc_hex_sqr(const uint8_t* a, uint8_t* out) {
+  Fp4 A[3];
+  hx_split(f12_in(a), A);
+  Fp ab[3][2], s[3][2], V[3][2];
+  Fp4h P[3][2], Q[3][2], T[3][2], R[3][2];
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) hx_sqr1(c, hx_view4(c, A[q]), ab[q][c], s[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) P[q][c] = hx_sqr2(c, ab[q][c], ab[q][c ^ 1], s[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) hx_sqr1(c, hx_view4(c, fp4_add(A[(q + 1) % 3], A[(q + 2) % 3])), ab[q][c], s[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) Q[q][c] = hx_sqr2(c, ab[q][c], ab[q][c ^ 1], s[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c)
+      hx_comb1(q, P[q][c], P[(q + 1) % 3][c], P[(q + 2) % 3][c], Q[SW12[q]][c], T[q][c], V[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c)
+      R[q][c] = hx_comb2(c, q, P[q][c], P[(q + 1) % 3][c], P[(q + 2) % 3][c], T[q][c], V[q][c], V[q][c ^ 1]);
+  f12_out(hx_join(R), out);
+}
+// f * line where line = (l0, l1, l4) each 96 bytes
+void hc_hex_line(const uint8_t* a, const uint8_t* l, uint8_t* out) {
+  Fp4 A[3];
+  hx_split(f12_in(a), A);
+  Fp2 l0 = {from_be(l), from_be(l + 48)}, l1 = {from_be(l + 96), from_be(l + 144)}, l4 = {from_be(l + 192), from_be(l + 240)};
+  HxLine r[3][2];
+  Fp4h R[3][2];
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) {
+      hx_line_u(c, hx_view4(c, A[(q + 1) % 3]), hx_view(c, l1), r[q][c]);
+      hx_line_t(c, q, hx_view4(c, A[q]), hx_view(c, l0), hx_view(c, l4), r[q][c]);
+    }
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) R[q][c] = hx_line2(c, q, r[q][c], r[q][c ^ 1].W);
+  f12_out(hx_join(R), out);
+}
+}
+
 #include "../../charon_amd/csrc/bls_lines.h"
 // Whole quad verify emulated on the host (same per-lane pieces as
 // k_verify_quad): lines precomputed with g2_lines, Miller accumulation and

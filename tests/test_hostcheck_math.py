@@ -256,6 +256,19 @@ def test_quad_lane_algebra_matches_tower():
     assert b2f12(call("hc_quad_cyc_sqr", f12b(f), out=576)) == bls.f12_sqr(f)
 
 
+def test_hex_lane_algebra_matches_tower():
+    """The hexad pieces (bls_hex.h: the trio with every Fp2 split over a lane
+    pair, the level-0 Miller kernel's layout), run as six emulated lanes,
+    equal the oracle's tower squaring and sparse line product."""
+    for _ in range(4):
+        a = rand_f12()
+        assert b2f12(call("hc_hex_sqr", f12b(a), out=576)) == bls.f12_sqr(a)
+        l0, l1, l4 = [(rng.randrange(P), rng.randrange(P)) for _ in range(3)]
+        line = ((l0, l1, bls.F2_ZERO), (bls.F2_ZERO, l4, bls.F2_ZERO))
+        got = b2f12(call("hc_hex_line", f12b(a), f2b(l0) + f2b(l1) + f2b(l4), out=576))
+        assert got == bls.f12_mul(a, line)
+
+
 def test_quad_verify_pipeline_emulated():
     """Line precomputation + quad Miller accumulation + quad final
     exponentiation (the k_lines_* / k_verify_quad algorithm) on the host."""
