@@ -37,15 +37,80 @@ __global__ void TBG_LAUNCH k_lagrange(DevBatch B) {
   for (int j = 0; j < 8; ++j) w[j] = lw[j];
 }
 
+// 96-byte compressed encoding of an affine point straight into the output
+// as 24 big-endian-packed words (the byte image of g2_compress, written with
+// word stores instead of a 96-byte stack array and byte stores).
+__device__ __forceinline__ void agg_store_compressed(const DevBatch& B, uint32_t d, const G2A& a) {
+  const Fp x0 = fp_from_mont(a.x.c0), x1 = fp_from_mont(a.x.c1);
+  const uint32_t flags = 0x80u | (fp2_lex_largest(a.y) ? 0x20u : 0u);
+  uint32_t* out = (uint32_t*)(B.agg + 96ull * d);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const Fp& x = h == 0 ? x1 : x0;
+#pragma unroll
+    for (int w = 0; w < 12; ++w) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // byte 4w + j of this half: bits 8 (47 - 4w - j)
+        const int bit = 8 * (47 - 4 * w - j);
+        const int li = bit / 28, off = bit % 28;
+        uint32_t b = x.l[li] >> off;
+        if (off > 20 && li + 1 < NL) b |= x.l[li + 1] << (28 - off);
+        v |= (b & 0xffu) << (8 * j);  // little-endian word of big-endian bytes
+      }
+      if (h == 0 && w == 0) v |= flags;
+      out[12 * h + w] = v;
+    }
+  }
+}
+__device__ __forceinline__ void agg_store_zero(const DevBatch& B, uint32_t d) {
+  uint32_t* out = (uint32_t*)(B.agg + 96ull * d);
+#pragma unroll
+  for (int w = 0; w < 24; ++w) out[w] = 0;
+}
+
 // Affine conversion, compression and status of a finished sum.
 __device__ void agg_emit(const DevBatch& B, uint32_t d, const G2J& acc) {
-  uint8_t* out = B.agg + 96ull * d;
   G2A a;
-  if (!jac_to_aff(acc, a)) { B.duty_status[d] = TBG_DS_AGG_IDENTITY; return; }
-  uint8_t enc[96];
-  g2_compress(a, false, enc);
-  for (int j = 0; j < 96; ++j) out[j] = enc[j];
+  if (!jac_to_aff(acc, a)) {
+    agg_store_zero(B, d);
+    B.duty_status[d] = TBG_DS_AGG_IDENTITY;
+    return;
+  }
+  agg_store_compressed(B, d, a);
   B.duty_status[d] = TBG_DS_OK;
+}
+
+// Integer-mode combination for duties of at most 32 partials, inline: the
+// participants as a bitmask, sum_j N_j P_j by double-and-add over the few
+// bits of |N_j| (3-of-4: 2 bits) with the point bodies in the kernel's own
+// code -- no out-of-line tss_combine call and no 256-byte mask on the stack.
+template <bool SPEC>
+__device__ __forceinline__ G2J combine_int_small(const DevBatch& B, uint32_t first, uint32_t n, uint32_t pmask,
+                                                 uint64_t& D) {
+  int nbits = 0;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (!((pmask >> j) & 1u)) continue;
+    const uint32_t* w = B.lam + 8ull * (first + j);
+    const int b = bitlen_u64((uint64_t)w[0] | ((uint64_t)w[1] << 32));
+    nbits = nbits > b ? nbits : b;
+  }
+  G2J acc = jac_inf<Fp2>();
+  for (int bit = nbits - 1; bit >= 0; --bit) {
+    acc = jac_dbl_in(acc);
+    for (uint32_t j = 0; j < n; ++j) {
+      if (!((pmask >> j) & 1u)) continue;
+      const uint32_t* w = B.lam + 8ull * (first + j);
+      const uint64_t mag = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      if (!((mag >> bit) & 1)) continue;
+      G2A p = B.sig_aff[first + j];
+      if (w[7] & 1) p.y = fp2_reduce(fp2_neg(p.y));
+      acc = jac_add_aff_in(acc, p);
+    }
+  }
+  const uint32_t* w0 = B.lam + 8ull * (first + (uint32_t)__builtin_ctz(pmask));
+  D = (uint64_t)w0[2] | ((uint64_t)w0[3] << 32);
+  return acc;
 }
 
 // Duties whose participants' integer Lagrange coefficients share a
@@ -58,8 +123,7 @@ __device__ void agg_emit(const DevBatch& B, uint32_t d, const G2J& acc) {
 template <bool SPEC>
 __device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& emit) {
   emit = false;
-  uint8_t* out = B.agg + 96ull * d;
-  for (int j = 0; j < 96; ++j) out[j] = 0;
+  agg_store_zero(B, d);
   uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
   uint32_t n = last - first;
   if (B.op == TBG_OP_VERIFY) return TBG_DS_NOT_AGGREGATED;
@@ -88,10 +152,17 @@ __device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& em
         return TBG_DS_AGG_DUPLICATE_ID;
     }
   }
-  uint8_t mask[256];
-  for (uint32_t j = first; j < last; ++j) mask[j - first] = participates<SPEC>(B.op, B.partial_status[j]) ? 1 : 0;
   uint64_t D = 1;
-  acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
+  uint32_t pmask = 0;
+  for (uint32_t j = first; j < last && j - first < 32; ++j)
+    if (participates<SPEC>(B.op, B.partial_status[j])) pmask |= 1u << (j - first);
+  if (n <= 32 && (B.lam[8ull * (first + (uint32_t)__builtin_ctz(pmask)) + 7] & LAM_INT_FLAG)) {
+    acc = combine_int_small<SPEC>(B, first, n, pmask, D);
+  } else {  // mod-r coefficients or more than 32 partials: the general form
+    uint8_t mask[256];
+    for (uint32_t j = first; j < last; ++j) mask[j - first] = participates<SPEC>(B.op, B.partial_status[j]) ? 1 : 0;
+    acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
+  }
   if (D > 1) {
     B.agg_acc[d] = acc;
     B.agg_list[atomicAdd(&B.counters[CNT_AGG], 1u)] = d;
@@ -120,10 +191,7 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_aggregate(DevBatch B) {
     B.duty_status[d] = TBG_DS_AGG_IDENTITY;
     return;
   }
-  uint8_t enc[96];
-  g2_compress(a, false, enc);
-  uint8_t* out = B.agg + 96ull * d;
-  for (int j = 0; j < 96; ++j) out[j] = enc[j];
+  agg_store_compressed(B, d, a);
   B.duty_status[d] = TBG_DS_OK;
 }
 

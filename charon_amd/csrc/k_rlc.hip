@@ -81,7 +81,8 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_rlc_duty_sum(DevBatch B) {
   if (in) {
     for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) {
       if (!rlc_candidate(B, i)) continue;
-      P = jac_add(P, B.part_p[i]);
+      // (G1 sums inline: the out-of-line form passes 3 x 2 Fp through scratch per addition)
+      P = jac_add_in<Fp, true>(P, B.part_p[i]);
       if (phase == DSUM_BOTH) S = jac_add(S, B.part_s[i]);
       ++cand;
     }
