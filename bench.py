@@ -421,6 +421,8 @@ def main():
     flat = [x for g in batches for x in g]
     group_used = e.stats(tickets[0])["group_size"]  # before api_pipeline reuses the slots (tickets expire)
     l0_state = e.level0(tickets[0])
+    fallback = e.fallback(tickets[0])  # per-level fallback work of the slot's last run
+    slot_dev, slot_pinned = e.slot_bytes(tickets[0])
 
     units = args.dvs * args.steps * ws
     value = units / elapsed
@@ -452,6 +454,8 @@ def main():
                    "rlc_group": group_used,
                    "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
+        "fallback_levels": fallback,
+        "slot_bytes": {"device": int(slot_dev), "pinned_host": int(slot_pinned), "batches_per_slot": M},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),
         "api_pipeline": api,

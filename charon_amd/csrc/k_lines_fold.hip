@@ -29,6 +29,9 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
   } else if (KIND == FOLD_CID) {
     if (k >= B.counters[CNT_CID] || !fb_in_pass(B, k) || (B.cid_list[k] & ID_DEGENERATE)) return;
     out = B.cid_lines;
+  } else if (KIND == FOLD_GID) {
+    if (k >= B.counters[CNT_GID] || !fb_in_pass(B, k) || (B.gid_list[k] & ID_DEGENERATE)) return;
+    out = B.gid_lines;
   } else if (KIND == FOLD_IDENT) {
     if (k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k) || (B.id_list[k] & ID_DEGENERATE)) return;
     out = B.id_lines;
@@ -51,6 +54,7 @@ void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStr
     case FOLD_CHUNKS: TBG_KLAUNCH(k_lines_fold<FOLD_CHUNKS>, grid, dim3(kBlock), st, B); break;
     case FOLD_CID: TBG_KLAUNCH(k_lines_fold<FOLD_CID>, grid, dim3(kBlock), st, B); break;
     case FOLD_L0: TBG_KLAUNCH(k_lines_fold<FOLD_L0>, grid, dim3(kBlock), st, B); break;
+    case FOLD_GID: TBG_KLAUNCH(k_lines_fold<FOLD_GID>, grid, dim3(kBlock), st, B); break;
     default: TBG_KLAUNCH(k_lines_fold<FOLD_IDENT>, grid, dim3(kBlock), st, B); break;
   }
 }

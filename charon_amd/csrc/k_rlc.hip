@@ -53,6 +53,16 @@ __device__ __forceinline__ bool rlc_candidate(const DevBatch& B, uint32_t i) {
   return B.partial_status[i] == TBG_PS_NOT_VERIFIED;
 }
 
+// A duty that level 1.5 / 2 may combine: COMBINED and its H(m) usable.
+__device__ __forceinline__ bool rlc_combinable(const DevBatch& B, uint32_t d) {
+  return B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] == 0;
+}
+__device__ __forceinline__ uint32_t rlc_candidates(const DevBatch& B, uint32_t d) {
+  uint32_t n = 0;
+  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) n += rlc_candidate(B, i) ? 1u : 0u;
+  return n;
+}
+
 // ------------------------------------------------------------------ level 0
 // [r_i] s_i and [r_i] pk_i: k_rlc_g2_pair / k_rlc_g1 (k_pair.hip).
 
@@ -276,6 +286,23 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
   for (uint32_t c = 1; c < nq; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
   f = quad_final_exp_in(quad_conj(f));
   bool ok = quad_is_one(f);
+  if (!ok && B.gident) {
+    // level 1g: the group's value A_g, and the group in the list (quad-uniform)
+    uint32_t m = 0;
+    for (uint32_t d = d0; d < d1; ++d)
+      if (rlc_combinable(B, d)) m += rlc_candidates(B, d);
+    if (m >= 2) {
+      uint32_t slot = 0;
+      if (lead) slot = atomicAdd(&B.counters[CNT_GID], 1u);
+      slot = (uint32_t)__shfl((int)slot, (int)quad_lead_lane());
+      quad_store(B.grp_fe + (size_t)3 * QUAD_WORDS * slot, f);
+      if (lead) {
+        B.gid_list[slot] = g;
+        B.grp_state[g] = GRP_GID;
+      }
+      return;
+    }
+  }
   if (lead) B.grp_state[g] = ok ? GRP_OK : GRP_FAIL;
 }
 
@@ -363,10 +390,6 @@ __device__ __forceinline__ void rlc_push_partials(const DevBatch& B, uint32_t d)
     if (rlc_candidate(B, i)) B.part_list[atomicAdd(&B.counters[CNT_PARTIALS], 1u)] = i;
 }
 
-// A duty that level 1.5 / 2 may combine: COMBINED and its H(m) usable.
-__device__ __forceinline__ bool rlc_combinable(const DevBatch& B, uint32_t d) {
-  return B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] == 0;
-}
 
 // After level 1 (one thread per duty): accept, split into level 1.5 (the
 // failed group's chunks), or go to level 3.
@@ -381,6 +404,7 @@ __global__ void TBG_LAUNCH k_rlc_resolve_groups(DevBatch B) {
   const uint32_t g = d / G;
   int32_t gs = B.grp_state[g];
   if (gs == GRP_OK) { rlc_mark(B, d, TBG_PS_VALID); return; }
+  if (gs == GRP_GID) return;  // level 1g resolves it (or hands its chunks to level 1.5)
   if (G == 1) { rlc_push_partials(B, d); return; }
   // the chunk goes to level 1.5 once: pushed by its first combinable duty
   const uint32_t c = (d - g * G) / C, dc0 = g * G + c * C;
@@ -410,11 +434,6 @@ __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
   B.pend_pts[k] = Sa;  // lines: k_lines_fold<FOLD_CHUNKS>
 }
 
-__device__ __forceinline__ uint32_t rlc_candidates(const DevBatch& B, uint32_t d) {
-  uint32_t n = 0;
-  for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) n += rlc_candidate(B, i) ? 1u : 0u;
-  return n;
-}
 
 // The fallback checks run their Miller loops and final exponentiations with
 // the squarings / line products inline (no scratch-stack call per step), as
@@ -670,6 +689,132 @@ __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
   }
 }
 
+// ------------------------------------------------------------ level 1g
+// The exponent test over a failed GROUP's candidates (members = partials,
+// w_i = the candidate's rank in the group, A = the group's value from
+// k_rlc_group_final): with exactly one bad partial -- most failed groups at
+// realistic invalid rates -- it is found with ONE more check instead of the
+// three levels 1.5 / 1.5b / 2b (each a final exponentiation deep).  A group
+// the test cannot resolve hands its chunks to level 1.5 as before.
+
+// Level 1g lines, one thread per entry: S' = sum w_i r_i s_i over the group
+// (suffix sums from its end), and per combinable duty
+// P'_d = sum_(i in d) w_i r_i pk_i = [o_d] sum p_i + sum_j j p_j (o_d: the
+// candidates before d; the second sum by suffix sums), affine as (-x, y).
+__global__ void TBG_LAUNCH k_rlc_gident_lines(DevBatch B) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= B.counters[CNT_GID]) return;
+  const uint32_t G = B.rlc_group, g = B.gid_list[k];
+  const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
+  G2J T = jac_inf<Fp2>(), U = jac_inf<Fp2>();
+  for (uint32_t d = d1; d-- > d0;) {
+    if (!rlc_combinable(B, d)) continue;
+    for (uint32_t i = B.duty_first[d + 1]; i-- > B.duty_first[d];) {
+      if (!rlc_candidate(B, i)) continue;
+      T = jac_add(T, B.part_s[i]);
+      U = jac_add(U, T);
+    }
+  }
+  G2A Sa;
+  bool ok = jac_to_aff(U, Sa);
+  uint32_t o = 0, r = 0;
+  for (uint32_t d = d0; d < d1 && ok; ++d) {
+    if (!rlc_combinable(B, d)) continue;
+    G1J Tp = jac_inf<Fp>(), Up = jac_inf<Fp>();
+    uint32_t n = 0;
+    for (uint32_t i = B.duty_first[d + 1]; i-- > B.duty_first[d];) {
+      if (!rlc_candidate(B, i)) continue;
+      Tp = jac_add_in<Fp, true>(Tp, B.part_p[i]);
+      Up = jac_add_in<Fp, true>(Up, Tp);
+      ++n;
+    }
+    if (o) Up = jac_add_in<Fp, true>(Up, jac_mul_u64(Tp, o));
+    G1A wp;
+    ok = jac_to_aff(Up, wp);
+    wp.x = fp_reduce(fp_neg(wp.x));
+    B.gid_p[(size_t)G * k + r++] = wp;
+    o += n;
+  }
+  if (!ok) {
+    B.gid_list[k] = g | ID_DEGENERATE;
+    return;
+  }
+  B.pend_pts[k] = Sa;  // lines: k_lines_fold<FOLD_GID>
+}
+
+// The chunks of group g with a combinable duty, to level 1.5 (as
+// k_rlc_resolve_groups lists those of a group level 1g does not take).
+__device__ __forceinline__ void push_group_chunks(const DevBatch& B, uint32_t g) {
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C;
+  for (uint32_t c = 0; c < nch; ++c) {
+    const uint32_t dc0 = g * G + c * C, dc1 = min(min(dc0 + C, g * G + G), B.n_duties);
+    for (uint32_t d = dc0; d < dc1; ++d)
+      if (rlc_combinable(B, d)) {
+        B.chunk_list[atomicAdd(&B.counters[CNT_CHUNKS], 1u)] = g * nch + c;
+        break;
+      }
+  }
+}
+
+// Level 1g check: one quad per entry computes A'_g over the group's
+// combinable duties and tests A_g^w == A'_g.  Found -> candidate w invalid,
+// the group's other candidates valid; not found (two or more bad partials)
+// or degenerate -> the group's chunks go to level 1.5.
+__global__ void TBG_LAUNCH k_rlc_gident_check(DevBatch B) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = fp12_slot(t) + B.fb_base;
+  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_GID] || !fb_in_pass(B, k)) return;
+  const bool lead = quad_lane() == 0;
+  const uint32_t G = B.rlc_group, entry = B.gid_list[k], g = entry & ~ID_DEGENERATE;
+  const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
+  uint32_t found = 0;
+  if (!(entry & ID_DEGENERATE)) {
+    uint32_t m = 0;
+    for (uint32_t d = d0; d < d1; ++d)
+      if (rlc_combinable(B, d)) m += rlc_candidates(B, d);
+    const uint32_t* ls = B.gid_lines + fb_slot(B, k);
+    const G1A* wp = B.gid_p + (size_t)G * k;
+    Fp4 f = quad_one();
+    int idx = 0;
+    for (int b = 62; b >= 0; --b) {
+      if (b != 62) f = FB_SQR(f);
+      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+      for (int s = 0; s < steps; ++s, ++idx) {
+        f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
+        uint32_t r = 0;
+        for (uint32_t d = d0; d < d1; ++d) {
+          if (!rlc_combinable(B, d)) continue;
+          const G1A& P = wp[r++];
+          f = quad_line_at<TBG_FALLBACK_INL>(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
+        }
+      }
+    }
+    const Fp4 inv_a2 = FB_FE(f);  // (A'_g)^-1
+    const Fp4 A = quad_load(B.grp_fe + (size_t)3 * QUAD_WORDS * k);
+    Fp4 Aw = A;
+    for (uint32_t w = 1; w <= m; ++w) {  // quad-uniform
+      if (quad_is_one(quad_mul(Aw, inv_a2))) {
+        found = w;
+        break;
+      }
+      Aw = quad_mul(Aw, A);
+    }
+  }
+  if (!lead) return;
+  if (!found) {
+    push_group_chunks(B, g);
+    return;
+  }
+  uint32_t w = 0;
+  for (uint32_t d = d0; d < d1; ++d) {
+    if (!rlc_combinable(B, d)) continue;
+    for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i) {
+      if (!rlc_candidate(B, i)) continue;
+      B.partial_status[i] = ++w == found ? TBG_PS_INVALID : TBG_PS_VALID;
+    }
+  }
+}
+
 // Per-partial schedule (TBG_VERIFY_EACH): every candidate goes to level 3.
 __global__ void TBG_LAUNCH k_list_all_partials(DevBatch B, const int32_t* pk_status, uint32_t n_pk) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -796,6 +941,12 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     TBG_KLAUNCH(k_rlc_group_final, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
+      // level 1g before the chunks: its unresolved groups add to the chunk list
+      TBG_KLAUNCH(k_rlc_gident_lines, grid_for(n_groups), dim3(kBlock), st, B);
+      fb_passes(B, n_groups, [&](const DevBatch& P, uint32_t n) {
+        launch_lines_fold(P, FOLD_GID, n, st);
+        TBG_KLAUNCH(k_rlc_gident_check, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+      });
       TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
       fb_passes(B, n_groups * nch, [&](const DevBatch& P, uint32_t n) {
         launch_lines_fold(P, FOLD_CHUNKS, n, st);

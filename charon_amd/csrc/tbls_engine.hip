@@ -557,6 +557,9 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_cidl = sec(G > 1 ? 4ull * ng * nch : 0);
   size_t w_cidp = sec(G > 1 ? sizeof(G1A) * (size_t)ng * nch * C : 0);
 
+  size_t w_gfe = sec(G > 1 ? 4ull * 3 * 4 * NL * ng : 0);
+  size_t w_gidl = sec(G > 1 ? 4ull * ng : 0);
+  size_t w_gidp = sec(G > 1 ? sizeof(G1A) * (size_t)ng * G : 0);
   size_t w_idl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_idp = sec(G > 1 ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_mr = sec(l0 ? 8ull * np : 0);
@@ -661,7 +664,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
     return code;
   };
   if (hipSetDevice(c->device) != hipSuccess) return release(TBG_E_DEVICE);
-  DevBatch B;
+  DevBatch B{};
   memset(&B, 0, sizeof(B));
   B.op = op;
   B.n_duties = nd;
@@ -725,6 +728,15 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.cid_list = (uint32_t*)(dw + w_cidl);
   B.cid_p = (G1A*)(dw + w_cidp);
   B.cid_lines = B.sig_lines;
+  static const uint32_t gident = [] {  // A/B knob: TBG_GIDENT=0 sends failed groups straight to level 1.5
+    const char* e = getenv("TBG_GIDENT");
+    return e ? (uint32_t)(atoi(e) != 0) : 1u;
+  }();
+  B.gident = G > 1 ? gident : 0u;
+  B.grp_fe = (uint32_t*)(dw + w_gfe);
+  B.gid_list = (uint32_t*)(dw + w_gidl);
+  B.gid_p = (G1A*)(dw + w_gidp);
+  B.gid_lines = B.sig_lines;
   B.id_list = (uint32_t*)(dw + w_idl);
   B.id_p = (G1A*)(dw + w_idp);
   B.id_lines = B.sig_lines;
@@ -998,6 +1010,40 @@ int tbg_fetch_stats(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
   return TBG_OK;
 }
 
+int tbg_fetch_fallback(tbg_ctx* c, tbg_ticket t, uint32_t* out8) {
+  if (!c || !out8) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = find_ticket(c, t, false, nullptr);
+  if (!s) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  uint32_t cnt[CNT_WORDS] = {};
+  if (s->op != TBG_OP_AGGREGATE) {
+    HIP_TRY(hipMemcpyAsync(cnt, s->B.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
+    HIP_TRY(hipStreamSynchronize(s->st));
+  }
+  out8[0] = s->B.rlc_group ? (s->n_duties + s->B.rlc_group - 1) / s->B.rlc_group : 0;
+  out8[1] = cnt[CNT_GID];
+  out8[2] = cnt[CNT_CHUNKS];
+  out8[3] = cnt[CNT_CID];
+  out8[4] = cnt[CNT_DUTIES];
+  out8[5] = cnt[CNT_PARTIALS];
+  out8[6] = s->B.rlc_group;
+  out8[7] = s->op == TBG_OP_AGGREGATE || !s->B.rlc_batch ? (uint32_t)TBG_L0_NOT_RUN
+            : cnt[CNT_L0_OK]                              ? (uint32_t)TBG_L0_PASSED
+                                                          : (uint32_t)TBG_L0_FAILED;
+  return TBG_OK;
+}
+
+int tbg_slot_bytes(tbg_ctx* c, tbg_ticket t, uint64_t* device_bytes, uint64_t* pinned_bytes) {
+  if (!c || !device_bytes || !pinned_bytes) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = find_ticket(c, t, false, nullptr);
+  if (!s) return TBG_E_TICKET;
+  *device_bytes = (uint64_t)s->d_in_cap + (uint64_t)s->d_work_cap;
+  *pinned_bytes = (uint64_t)s->h_in_cap + (uint64_t)s->h_out_cap;
+  return TBG_OK;
+}
+
 int tbg_fetch_level0(tbg_ctx* c, tbg_ticket t, int32_t* state) {
   if (!c || !state) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1079,7 +1125,7 @@ int tbg_sign(tbg_ctx* c, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, c
       hipMemcpyAsync(d_im, item_msg, 4ull * n, hipMemcpyHostToDevice, st) != hipSuccess)
     rc = TBG_E_DEVICE;
   if (rc == TBG_OK) {
-    DevBatch B;
+    DevBatch B{};
     memset(&B, 0, sizeof(B));
     B.n_msgs = n_msgs;
     B.msgs = d_msgs;
@@ -1260,7 +1306,7 @@ int tbg_fast_aggregate_verify(tbg_ctx* c, const uint32_t* pubkey_ids, const uint
   tbg::launch_sum_g1(c->d_pk, c->d_pk_status, c->n_pk, d_ids, p, d_pk48, d_kst, st);
   tbg::launch_decode_pubkeys(d_pk48, n, t_pk, t_xpk, t_pkst, st);  // a failed / identity sum: not DEC_OK
   // 2. one CoreVerify per set against that table (the per-item schedule)
-  DevBatch B;
+  DevBatch B{};
   memset(&B, 0, sizeof(B));
   B.op = TBG_OP_VERIFY;
   B.n_duties = B.n_partials = B.n_msgs = n;

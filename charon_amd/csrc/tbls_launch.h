@@ -83,6 +83,13 @@ struct DevBatch {
   uint32_t* cid_list;     // [n_groups * chunks] level-1.5b entries: chunk-list positions
   G1A* cid_p;             // [n_groups * chunks][rlc_chunk] w_d P_d as (-x, y), by level-1.5b position
   uint32_t* cid_lines;    // [fb window][LINES_WORDS] lines of sum w_d S_d, by level-1.5b position - fb_base
+  // level 1g: the exponent test over a failed GROUP's partials, right after
+  // level 1 (most failed groups hold exactly one bad partial)
+  uint32_t gident;        // 1: failed groups go to level 1g first (0: straight to level 1.5)
+  uint32_t* grp_fe;       // [n_groups][3][4 NL] final-exponentiated value A_g of a level-1g group (by list position)
+  uint32_t* gid_list;     // [n_groups] level-1g entries: group index (| ID_DEGENERATE)
+  G1A* gid_p;             // [n_groups][rlc_group] sum_(i in d) w_i r_i pk_i as (-x, y), by level-1g position
+  uint32_t* gid_lines;    // lines of sum w_i r_i sig_i by level-1g position - fb_base (the fallback line buffer)
   uint32_t* id_fe;        // [n_duties][3][4 NL] value A_d of each level-2b duty (by list position)
   uint32_t* id_list;      // [n_duties] level-2b entries: failed duties with several candidates
   G1A* id_p;              // [n_duties] sum w_i r_i pk_i (affine), by level-2b position
@@ -121,12 +128,12 @@ struct DevBatch {
 };
 
 enum RlcState : int32_t { RLC_NONE = 0, RLC_COMBINED = 1, RLC_EACH = 2 };
-enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3 };
+enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL = 3, GRP_GID = 4 };  // GRP_GID: at level 1g
 // CNT_DUTIES: level-2b duties (id_list), CNT_PARTIALS: level-3 partials, CNT_AGG: [1/D] duties,
 // CNT_CHUNKS: level-1.5 chunks, CNT_CID: level-1.5b chunks, CNT_L0_BAD: level 0 cannot
 // hold (a degenerate sum, a duty checked per partial, an unusable H(m)), CNT_L0_OK: level 0 passed
 enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_CID = 4, CNT_L0_BAD = 5,
-                     CNT_L0_OK = 6, CNT_WORDS = 7 };
+                     CNT_L0_OK = 6, CNT_GID = 7, CNT_WORDS = 8 };  // CNT_GID: level-1g groups
 
 // Level-0 MSM: a digit a (odd, |a| < 2^16) of r_i puts psi^k(s_i) into bucket
 // (|a| - 1) / 2; the tree sums fold MSM_SUM_FAN points per thread.
@@ -151,7 +158,7 @@ enum DutySumPhase : int { DSUM_BOTH = 0, DSUM_L0_P = 1, DSUM_FALLBACK_S = 2 };
 constexpr uint32_t CHUNK_DEGENERATE = 0x80000000u;
 constexpr uint32_t ID_DEGENERATE = 0x80000000u;
 // k_lines_fold<KIND>: which pending points get lines, and where they go.
-enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3, FOLD_L0 = 4 };
+enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3, FOLD_L0 = 4, FOLD_GID = 5 };
 
 // Fallback list position k in the current pass, and its slot in the line buffer.
 TBG_HD bool fb_in_pass(const DevBatch& B, uint32_t k) { return B.fb_window == 0 || k - B.fb_base < B.fb_window; }

@@ -222,6 +222,19 @@ class Engine:
         self._check(self._lib.tbg_fetch_stats(self._h, ticket, _ptr(out)), "tbg_fetch_stats")
         return dict(zip(["groups", "duty_checks", "partial_checks", "group_size"], out.tolist()))
 
+    def fallback(self, ticket) -> dict:
+        """Work per verification level of the batch's last run (tbg_fetch_fallback)."""
+        out = np.zeros(8, dtype=np.uint32)
+        self._check(self._lib.tbg_fetch_fallback(self._h, ticket, _ptr(out)), "tbg_fetch_fallback")
+        return dict(zip(["groups", "group_searches", "chunks", "chunk_searches", "duty_searches", "partial_checks",
+                         "group_size", "level0"], out.tolist()))
+
+    def slot_bytes(self, ticket) -> tuple:
+        """(device bytes, pinned host bytes) of the slot holding the ticket's batch."""
+        dev, pin = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self._lib.tbg_slot_bytes(self._h, ticket, ctypes.byref(dev), ctypes.byref(pin)), "tbg_slot_bytes")
+        return dev.value, pin.value
+
     def level0(self, ticket) -> int:
         """Level 0 of the batch's last run: L0_NOT_RUN, L0_PASSED or L0_FAILED."""
         st = ctypes.c_int32(0)

@@ -218,6 +218,15 @@ int tbg_fetch_stats(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out4);
  * TBG_L0_PASSED (every candidate accepted by the one batch-wide check) or
  * TBG_L0_FAILED (the group levels decided). */
 int tbg_fetch_level0(tbg_ctx* ctx, tbg_ticket ticket, int32_t* state);
+/* Fallback work of a collected batch's last run, per level: out8 = [level-1
+ * groups, groups searched at level 1g (exponent test over a failed group's
+ * partials), chunks re-checked at level 1.5, chunks searched at level 1.5b,
+ * duties searched at level 2b, partials checked one by one at level 3,
+ * duties per group, level 0 (TBG_L0_*)]. */
+int tbg_fetch_fallback(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out8);
+/* Footprint of the slot holding the ticket's batch: device bytes (input
+ * arena + work arena) and pinned host bytes (staging both ways). */
+int tbg_slot_bytes(tbg_ctx* ctx, tbg_ticket ticket, uint64_t* device_bytes, uint64_t* pinned_bytes);
 
 /* Plain BLS aggregation (every coefficient 1) for the DKG / cluster-lock
  * multi-signatures: AggregatePublicKeys / AggregateSignatures of

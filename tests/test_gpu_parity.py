@@ -308,3 +308,31 @@ def test_level0_pass_and_fall_through():
             assert after == (eng.L0_PASSED if cfg else eng.L0_NOT_RUN)
         finally:
             e.close()
+
+
+def test_level1g_resolves_single_bad_partials():
+    """Level 1g: a failed group holding ONE bad partial is resolved by the
+    exponent test over the group's partials (no chunk, duty or per-partial
+    level), with verdicts and aggregates exact; groups with several bad
+    partials still reach the deeper levels and come out exact too."""
+    from charon_amd import engine as eng
+    e = eng.Engine(0, verify_mode=0, rlc_group=8, rlc_chunk=4, rlc_batch=2, rlc_seed=0x1A)
+    try:
+        b = _make_cluster_batch(e, 2000, 3, 4, seed=23, inject=0.01)
+        t = e.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
+                     duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+        res = e.collect(t)
+        assert np.array_equal(res.partial_status == eng.PS_VALID, ~b.injected)
+        ok = res.duty_status == eng.DS_OK
+        assert np.array_equal(ok, b.expect_ok)
+        assert np.array_equal(res.agg[ok], b.group_sig[ok])
+        fb = e.fallback(t)
+        bad_groups = {int(i) // (4 * 8) for i in np.flatnonzero(b.injected)}
+        multi = sum(1 for g in bad_groups if int(b.injected[32 * g:32 * g + 32].sum()) > 1)
+        assert fb["group_size"] == 8 and fb["group_searches"] == len(bad_groups), (fb, len(bad_groups))
+        # only groups with two or more bad partials go deeper (their chunks)
+        assert fb["chunks"] <= 2 * multi, (fb, multi)
+        dev, pinned = e.slot_bytes(t)
+        assert dev > 0 and pinned > 0
+    finally:
+        e.close()
