@@ -120,20 +120,22 @@ STAGE_KERNELS = {
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
                 "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>"],
     "h_lines": ["k_lines_h"],
-    "verify": ["k_l0_miller_hex", "k_rlc_miller_chunks<MILLER_L0>", "k_rlc_miller_chunks<MILLER_GROUP_S>",
+    "verify": ["k_miller_hex<MILLER_L0>", "k_miller_hex<MILLER_GROUPS>", "k_rlc_miller_chunks<MILLER_L0>", "k_rlc_miller_chunks<MILLER_GROUP_S>",
                "k_rlc_miller_chunks<MILLER_GROUPS>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after",
-               "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_chunk_lines", "k_lines_fold<FOLD_CHUNKS>",
+               "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_gident_lines", "k_lines_fold<FOLD_GID>",
+               "k_rlc_gident_miller", "k_rlc_gident_check", "k_rlc_chunk_lines", "k_lines_fold<FOLD_CHUNKS>",
                "k_rlc_check_chunks", "k_rlc_cident_lines", "k_lines_fold<FOLD_CID>", "k_rlc_cident_check",
                "k_rlc_ident_lines", "k_lines_fold<FOLD_IDENT>", "k_rlc_ident_check", "k_lines_sig_list",
                "k_verify_list"],
     # (the speculative pass <true> runs mid-chain while level 0 is on; the
     # regular pass <false> then returns at once after a level-0 pass)
-    "aggregate": ["k_lagrange<true>", "k_aggregate<true>", "k_aggregate_finish<true>", "k_lagrange<false>",
-                  "k_aggregate<false>", "k_aggregate_finish<false>"],
+    "aggregate": ["k_lagrange<true>", "k_aggregate<true>", "k_aggregate_finish<true>", "k_aggregate_exc<true>",
+                  "k_lagrange<false>", "k_aggregate<false>", "k_aggregate_finish<false>", "k_aggregate_exc<false>"],
 }
 # profile name (launch site) -> the symbol rocprofv3 prints for it
 ROCPROF_NAME = {
-    "k_l0_miller_hex": "tbg::k_l0_miller_hex(tbg::DevBatch)",
+    "k_miller_hex<MILLER_L0>": "void tbg::k_miller_hex<1>(tbg::DevBatch)",
+    "k_miller_hex<MILLER_GROUPS>": "void tbg::k_miller_hex<0>(tbg::DevBatch)",
     "k_rlc_miller_chunks<MILLER_L0>": "void tbg::k_rlc_miller_chunks<1>(tbg::DevBatch)",
     "k_rlc_miller_chunks<MILLER_GROUP_S>": "void tbg::k_rlc_miller_chunks<2>(tbg::DevBatch)",
     "k_rlc_miller_chunks<MILLER_GROUPS>": "void tbg::k_rlc_miller_chunks<0>(tbg::DevBatch)",

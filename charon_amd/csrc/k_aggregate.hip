@@ -3,6 +3,7 @@
 #include "tbls_launch.h"
 #include "bls_tss.h"
 #include "bls_batchinv.h"
+#include "bls_pair.h"
 
 namespace tbg {
 
@@ -195,24 +196,30 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_aggregate(DevBatch B) {
   B.duty_status[d] = TBG_DS_OK;
 }
 
-__device__ __forceinline__ G2J shfl_xor_g2j(const G2J& a, int m) {
-  G2J r;
-  const Fp* src[6] = {&a.X.c0, &a.X.c1, &a.Y.c0, &a.Y.c1, &a.Z.c0, &a.Z.c1};
-  Fp* dst[6] = {&r.X.c0, &r.X.c1, &r.Y.c0, &r.Y.c1, &r.Z.c0, &r.Z.c1};
-  for (int k = 0; k < 6; ++k)
-    for (int j = 0; j < NL; ++j) dst[k]->l[j] = __shfl_xor(src[k]->l[j], m, 4);
+constexpr uint32_t AGG_EXC = 0x80000000u;  // agg_list flag: finish on the reference path
+
+// this lane's component of the same pair-form point on lane ^ m
+__device__ __forceinline__ Jac<Fp2x> shfl_xor_px(const Jac<Fp2x>& a, int m) {
+  Jac<Fp2x> r;
+  const Fp* src[3] = {&a.X.v, &a.Y.v, &a.Z.v};
+  Fp* dst[3] = {&r.X.v, &r.Y.v, &r.Z.v};
+  for (int k = 0; k < 3; ++k)
+    for (int j = 0; j < NL; ++j) dst[k]->l[j] = __shfl_xor(src[k]->l[j], m, 8);
   return r;
 }
 
-// [1/D] acc as the 4-way base-|x| MSM of bls_tss.h, one term per lane of a
-// quad (64 doublings each instead of 255 on one lane), summed over the quad.
+// [1/D] acc as the 4-way base-|x| MSM of bls_tss.h: EIGHT lanes per listed
+// duty, digit q = (lane >> 1) & 3 on a lane pair (bls_pair.h: each lane holds
+// one component of every Fp2, so the G2 loop fits two waves per SIMD -- the
+// single-lane form needed 768 registers and spilled 454), 64 doublings per
+// pair, summed over the four pairs.
 template <bool SPEC>
-__global__ void TBG_LAUNCH k_aggregate_finish(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_aggregate_finish(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t k = t >> 2;
-  const int q = (int)(t & 3);
+  const uint32_t k = t >> 3;
+  const int q = (int)((t >> 1) & 3);
   if (spec_skip(B, SPEC)) return;
-  if (k >= B.counters[CNT_AGG]) return;  // quad-uniform
+  if (k >= B.counters[CNT_AGG]) return;  // 8-lane uniform
   const uint32_t d = B.agg_list[k];
   uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
   uint32_t j = first;
@@ -222,15 +229,39 @@ __global__ void TBG_LAUNCH k_aggregate_finish(DevBatch B) {
   uint64_t dg[4];
   inv_den_digits(D, dg);
   const uint64_t e = q == 0 ? dg[0] : q == 1 ? dg[1] : q == 2 ? dg[2] : dg[3];
-  const G2J p = base_x_point(B.agg_acc[d], q);
-  G2J acc = jac_inf<Fp2>();
+  const Jac<Fp2x> p = px_load(base_x_point(B.agg_acc[d], q));
+  // additions without the doubling branch (bls_pair.h jac_add_x): a case that
+  // needs it (probability ~2^-250 per step) sets `exc` and the duty is
+  // finished on the single-lane reference path instead
+  bool exc = false;
+  Jac<Fp2x> acc = jac_inf<Fp2x>();
   for (int b = 63; b >= 0; --b) {
-    acc = jac_dbl_in(acc);
-    if ((e >> b) & 1) acc = jac_add_in<Fp2, true>(acc, p);
+    acc = jac_dbl_lo(acc);
+    if ((e >> b) & 1) acc = jac_add_x(acc, p, exc);
   }
-  acc = jac_add_in<Fp2, true>(acc, shfl_xor_g2j(acc, 1));
-  acc = jac_add_in<Fp2, true>(acc, shfl_xor_g2j(acc, 2));
-  if (q == 0) agg_emit(B, d, acc);
+  acc = jac_add_x(acc, shfl_xor_px(acc, 2), exc);
+  acc = jac_add_x(acc, shfl_xor_px(acc, 4), exc);
+  exc = __any(exc);  // (wave-wide: rare; the 8-lane group decides together)
+  if (q != 0) return;
+  if (exc) {
+    if (pair_par() == 0) B.agg_list[k] = d | AGG_EXC;  // k_aggregate_exc finishes it
+    return;
+  }
+  const G2J full = {px_gather(acc.X), px_gather(acc.Y), px_gather(acc.Z)};
+  if (pair_par() == 0) agg_emit(B, d, full);
+}
+
+// The listed duties whose pair-form ladder met the doubling case: the
+// single-lane reference form (one thread per list entry).
+template <bool SPEC>
+__global__ void TBG_LAUNCH k_aggregate_exc(DevBatch B) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (spec_skip(B, SPEC) || k >= B.counters[CNT_AGG] || !(B.agg_list[k] & AGG_EXC)) return;
+  const uint32_t d = B.agg_list[k] & ~AGG_EXC;
+  uint32_t j = B.duty_first[d];
+  while (j < B.duty_first[d + 1] && !participates<SPEC>(B.op, B.partial_status[j])) ++j;
+  const uint32_t* w = B.lam + 8ull * j;
+  agg_emit(B, d, tss_div_den(B.agg_acc[d], (uint64_t)w[2] | ((uint64_t)w[3] << 32)));
 }
 
 void launch_lagrange(const DevBatch& B, hipStream_t st, bool spec) {
@@ -246,8 +277,13 @@ void launch_aggregate(const DevBatch& B, hipStream_t st, bool spec) {
 }
 void launch_aggregate_finish(const DevBatch& B, hipStream_t st, bool spec) {
   if (!B.n_duties) return;
-  if (spec) TBG_KLAUNCH(k_aggregate_finish<true>, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
-  else TBG_KLAUNCH(k_aggregate_finish<false>, grid_for(4 * B.n_duties), dim3(kBlock), st, B);
+  if (spec) {
+    TBG_KLAUNCH(k_aggregate_finish<true>, grid_for(8 * B.n_duties), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_aggregate_exc<true>, grid_for(B.n_duties), dim3(kBlock), st, B);
+  } else {
+    TBG_KLAUNCH(k_aggregate_finish<false>, grid_for(8 * B.n_duties), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_aggregate_exc<false>, grid_for(B.n_duties), dim3(kBlock), st, B);
+  }
 }
 
 }  // namespace tbg

@@ -22,29 +22,40 @@ namespace tbg {
 #define TBG_HEX_WAVES 2
 #endif
 
-// One hexad per (group, chunk of rlc_chunk duties), then ONE hexad for level
-// 0's S pair (batch lines folded with -g1), as k_rlc_miller_chunks<MILLER_L0>.
-__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_l0_miller_hex(DevBatch B) {
+// One hexad per (group, chunk of rlc_chunk duties), then the S hexads, as
+// k_rlc_miller_chunks (k_rlc.hip):
+//   MILLER_L0      ONE S hexad for level 0's batch-wide S (batch lines, -g1 folded)
+//   MILLER_GROUPS  one S hexad per group (group lines); groups without
+//                  candidates skipped, a degenerate group S keeps its P chunks
+template <int MODE>
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_miller_hex(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk;
   const uint32_t n_groups = (B.n_duties + G - 1) / G;
   const uint32_t nch = (G + C - 1) / C, nq = nch + 1;
   const uint32_t np_q = n_groups * nch;
   const uint32_t qd = hex_slot(t);
-  if (qd == 0xFFFFFFFFu || qd >= np_q + 1) return;
-  const bool s_quad = qd == np_q;
-  const uint32_t* ls;
+  if (qd == 0xFFFFFFFFu || qd >= np_q + (MODE == MILLER_L0 ? 1u : n_groups)) return;
+  const bool s_quad = qd >= np_q;
+  const uint32_t* ls = nullptr;
   uint32_t* dst;
   uint32_t d0 = 0, d1 = 0;
-  if (s_quad) {
+  if (MODE == MILLER_L0 && s_quad) {
     if (B.counters[CNT_L0_BAD]) return;
     ls = B.batch_lines;
     dst = B.batch_f;
   } else {
-    const uint32_t g = qd / nch, c = qd % nch;
-    d0 = g * G + c * C;
-    d1 = min(d0 + C, min(g * G + G, B.n_duties));
-    ls = nullptr;
+    const uint32_t g = s_quad ? qd - np_q : qd / nch, c = s_quad ? nch : qd % nch;
+    if (MODE == MILLER_GROUPS) {
+      const int32_t gs = B.grp_state[g];
+      if (gs == GRP_EMPTY || (gs == GRP_FAIL && s_quad)) return;
+    }
+    if (s_quad) {
+      ls = B.grp_lines + (size_t)LINES_WORDS * g;
+    } else {
+      d0 = g * G + c * C;
+      d1 = min(d0 + C, min(g * G + G, B.n_duties));
+    }
     dst = B.chunk_f + (size_t)3 * 4 * NL * (g * nq + c);
   }
   Fp4h f = hex_one();
@@ -60,7 +71,7 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_l0_miller_hex(DevBatch B) {
       for (uint32_t d = d0; d < d1; ++d) {
         if (B.dv_state[d] != RLC_COMBINED) continue;
         const uint32_t m = B.duty_msg[d];
-        if (B.h_status[m] != 0) continue;  // level 0 fails in k_l0_fold
+        if (B.h_status[m] != 0) continue;  // the check fails in k_l0_fold / k_rlc_group_final
         const G1A& P = B.dv_p[d];
         f = hex_line_at(f, B.h_lines + (size_t)LINES_WORDS * m, idx, fp_reduce(fp_neg(P.x)), P.y);
       }
@@ -72,7 +83,12 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_l0_miller_hex(DevBatch B) {
 void launch_l0_miller_hex(const DevBatch& B, hipStream_t st) {
   const uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
   const uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
-  TBG_KLAUNCH(k_l0_miller_hex, grid_for(hex_threads(n_groups * nch + 1)), dim3(kBlock), st, B);
+  TBG_KLAUNCH(k_miller_hex<MILLER_L0>, grid_for(hex_threads(n_groups * nch + 1)), dim3(kBlock), st, B);
+}
+void launch_groups_miller_hex(const DevBatch& B, hipStream_t st) {
+  const uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
+  const uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
+  TBG_KLAUNCH(k_miller_hex<MILLER_GROUPS>, grid_for(hex_threads(n_groups * (nch + 1))), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

@@ -697,49 +697,69 @@ __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
 // three levels 1.5 / 1.5b / 2b (each a final exponentiation deep).  A group
 // the test cannot resolve hands its chunks to level 1.5 as before.
 
-// Level 1g lines, one thread per entry: S' = sum w_i r_i s_i over the group
-// (suffix sums from its end), and per combinable duty
-// P'_d = sum_(i in d) w_i r_i pk_i = [o_d] sum p_i + sum_j j p_j (o_d: the
-// candidates before d; the second sum by suffix sums), affine as (-x, y).
+// G2J / G1J of lane ^ m within groups of `width` lanes
+template <class P>
+__device__ __forceinline__ P shfl_xor_pt(const P& a, int m, int width) {
+  P r;
+  const uint32_t* src = (const uint32_t*)&a;
+  uint32_t* dst = (uint32_t*)&r;
+#pragma unroll
+  for (int j = 0; j < (int)(sizeof(P) / 4); ++j) dst[j] = (uint32_t)__shfl_xor((int)src[j], m, width);
+  return r;
+}
+
+// lanes per level-1g entry: the group size rounded up to a power of two (<= 64)
+__device__ __forceinline__ uint32_t gid_width(uint32_t G) { return G <= 1 ? 1u : 1u << (32 - __clz((int)(G - 1))); }
+
+// Level 1g lines, one LANE PER DUTY of the entry's group (a power-of-two run
+// of lanes): with n_d the candidates of duty d and o_d those ranked before it,
+//   P'_d = [o_d] sum_(i in d) p_i + sum_j j p_j   (p_i = r_i pk_i; suffix sums),
+//   S'   = sum_d ([o_d] sum_(i in d) s_i + sum_j j s_j)   (a shuffle tree),
+// o_d by a prefix scan over the lanes.  P'_d is stored by the duty's position
+// in the group as (-x, y); S' goes to pend_pts for its lines.
 __global__ void TBG_LAUNCH k_rlc_gident_lines(DevBatch B) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= B.counters[CNT_GID]) return;
-  const uint32_t G = B.rlc_group, g = B.gid_list[k];
-  const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
-  G2J T = jac_inf<Fp2>(), U = jac_inf<Fp2>();
-  for (uint32_t d = d1; d-- > d0;) {
-    if (!rlc_combinable(B, d)) continue;
+  const uint32_t G = B.rlc_group, W = gid_width(G);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, k = t / W, r = t % W;
+  if (k >= B.counters[CNT_GID]) return;  // (W-lane uniform)
+  const uint32_t g = B.gid_list[k], d = g * G + r;
+  const bool valid = r < G && d < B.n_duties && rlc_combinable(B, d);
+  G2J Xs = jac_inf<Fp2>(), Ys = jac_inf<Fp2>();
+  G1J Xp = jac_inf<Fp>(), Yp = jac_inf<Fp>();
+  uint32_t n = 0;
+  if (valid) {
     for (uint32_t i = B.duty_first[d + 1]; i-- > B.duty_first[d];) {
       if (!rlc_candidate(B, i)) continue;
-      T = jac_add(T, B.part_s[i]);
-      U = jac_add(U, T);
-    }
-  }
-  G2A Sa;
-  bool ok = jac_to_aff(U, Sa);
-  uint32_t o = 0, r = 0;
-  for (uint32_t d = d0; d < d1 && ok; ++d) {
-    if (!rlc_combinable(B, d)) continue;
-    G1J Tp = jac_inf<Fp>(), Up = jac_inf<Fp>();
-    uint32_t n = 0;
-    for (uint32_t i = B.duty_first[d + 1]; i-- > B.duty_first[d];) {
-      if (!rlc_candidate(B, i)) continue;
-      Tp = jac_add_in<Fp, true>(Tp, B.part_p[i]);
-      Up = jac_add_in<Fp, true>(Up, Tp);
+      Xs = jac_add(Xs, B.part_s[i]);
+      Ys = jac_add(Ys, Xs);
+      Xp = jac_add_in<Fp, true>(Xp, B.part_p[i]);
+      Yp = jac_add_in<Fp, true>(Yp, Xp);
       ++n;
     }
-    if (o) Up = jac_add_in<Fp, true>(Up, jac_mul_u64(Tp, o));
+  }
+  uint32_t o = n;  // inclusive scan of n over the run, then exclusive
+  for (uint32_t m = 1; m < W; m <<= 1) {
+    const uint32_t v = (uint32_t)__shfl_up((int)o, m, W);
+    if (r >= m) o += v;
+  }
+  o -= n;
+  bool ok = true;
+  if (valid) {
+    if (o) {
+      Yp = jac_add_in<Fp, true>(Yp, jac_mul_u64(Xp, o));
+      Ys = jac_add(Ys, jac_mul_u64(Xs, o));
+    }
     G1A wp;
-    ok = jac_to_aff(Up, wp);
+    ok = jac_to_aff(Yp, wp);
     wp.x = fp_reduce(fp_neg(wp.x));
-    B.gid_p[(size_t)G * k + r++] = wp;
-    o += n;
+    B.gid_p[(size_t)G * k + r] = wp;
   }
-  if (!ok) {
-    B.gid_list[k] = g | ID_DEGENERATE;
-    return;
+  for (uint32_t m = 1; m < W; m <<= 1) Ys = jac_add(Ys, shfl_xor_pt(Ys, (int)m, (int)W));
+  if (r == 0) {
+    G2A Sa;
+    if (jac_to_aff(Ys, Sa)) B.pend_pts[k] = Sa;  // lines: k_lines_fold<FOLD_GID>
+    else ok = false;
   }
-  B.pend_pts[k] = Sa;  // lines: k_lines_fold<FOLD_GID>
+  if (!ok) atomicOr(&B.gid_list[k], ID_DEGENERATE);
 }
 
 // The chunks of group g with a combinable duty, to level 1.5 (as
@@ -756,39 +776,67 @@ __device__ __forceinline__ void push_group_chunks(const DevBatch& B, uint32_t g)
   }
 }
 
-// Level 1g check: one quad per entry computes A'_g over the group's
-// combinable duties and tests A_g^w == A'_g.  Found -> candidate w invalid,
-// the group's other candidates valid; not found (two or more bad partials)
-// or degenerate -> the group's chunks go to level 1.5.
+// Level 1g Miller part, as level 1's: one quad per (entry, chunk of
+// rlc_chunk duties) over the duties' (P'_d, H(m_d)) pairs, and one quad per
+// entry for the S' pair (its folded lines), each product into gid_f.
+__global__ void TBG_LAUNCH k_rlc_gident_miller(DevBatch B) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C, nq = nch + 1;
+  const uint32_t s = fp12_slot(t);
+  if (s == 0xFFFFFFFFu) return;
+  const uint32_t k = s / nq + B.fb_base, c = s % nq;
+  if (k >= B.counters[CNT_GID] || !fb_in_pass(B, k)) return;
+  const uint32_t entry = B.gid_list[k];
+  if (entry & ID_DEGENERATE) return;
+  const uint32_t g = entry, gd0 = g * G, gd1 = min(gd0 + G, B.n_duties);
+  const uint32_t d0 = c == nch ? gd0 : min(gd0 + c * C, gd1), d1 = c == nch ? gd0 : min(d0 + C, gd1);
+  const uint32_t* ls = B.gid_lines + fb_slot(B, k);
+  const G1A* wp = B.gid_p + (size_t)G * k;
+  Fp4 f = quad_one();
+  int idx = 0;
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = FB_SQR(f);
+    int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+    for (int st = 0; st < steps; ++st, ++idx) {
+      if (c == nch) f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
+      for (uint32_t d = d0; d < d1; ++d) {
+        if (!rlc_combinable(B, d)) continue;
+        const G1A& P = wp[d - gd0];
+        f = quad_line_at<TBG_FALLBACK_INL>(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
+      }
+    }
+  }
+  quad_store(B.gid_f + (size_t)3 * QUAD_WORDS * ((size_t)k * nq + c), f);
+}
+
+// Candidates of an unresolved level-1g group up to which they all go to
+// level 3 directly (more: the group's chunks go to level 1.5).
+#ifndef TBG_GID_L3_MAX
+#define TBG_GID_L3_MAX 40u
+#endif
+
+// Level 1g check: one quad per entry multiplies its products into A'_g and
+// tests A_g^w == A'_g.  Found -> candidate w invalid, the group's other
+// candidates valid; not found (two or more bad partials) or degenerate ->
+// the group's candidates go to the exact per-partial level (the levels
+// between cost a final exponentiation of latency each whatever their list
+// length, profiles/r03/gident/) -- or, with TBG_GIDENT=2, its chunks to
+// level 1.5 as the round-2 order had them.
 __global__ void TBG_LAUNCH k_rlc_gident_check(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t k = fp12_slot(t) + B.fb_base;
   if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_GID] || !fb_in_pass(B, k)) return;
   const bool lead = quad_lane() == 0;
-  const uint32_t G = B.rlc_group, entry = B.gid_list[k], g = entry & ~ID_DEGENERATE;
+  const uint32_t G = B.rlc_group, C = B.rlc_chunk, nq = (G + C - 1) / C + 1;
+  const uint32_t entry = B.gid_list[k], g = entry & ~ID_DEGENERATE;
   const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
-  uint32_t found = 0;
+  uint32_t found = 0, m = 0;
+  for (uint32_t d = d0; d < d1; ++d)
+    if (rlc_combinable(B, d)) m += rlc_candidates(B, d);
   if (!(entry & ID_DEGENERATE)) {
-    uint32_t m = 0;
-    for (uint32_t d = d0; d < d1; ++d)
-      if (rlc_combinable(B, d)) m += rlc_candidates(B, d);
-    const uint32_t* ls = B.gid_lines + fb_slot(B, k);
-    const G1A* wp = B.gid_p + (size_t)G * k;
-    Fp4 f = quad_one();
-    int idx = 0;
-    for (int b = 62; b >= 0; --b) {
-      if (b != 62) f = FB_SQR(f);
-      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-      for (int s = 0; s < steps; ++s, ++idx) {
-        f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
-        uint32_t r = 0;
-        for (uint32_t d = d0; d < d1; ++d) {
-          if (!rlc_combinable(B, d)) continue;
-          const G1A& P = wp[r++];
-          f = quad_line_at<TBG_FALLBACK_INL>(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
-        }
-      }
-    }
+    const uint32_t* base = B.gid_f + (size_t)3 * QUAD_WORDS * ((size_t)k * nq);
+    Fp4 f = quad_load(base);
+    for (uint32_t c = 1; c < nq; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
     const Fp4 inv_a2 = FB_FE(f);  // (A'_g)^-1
     const Fp4 A = quad_load(B.grp_fe + (size_t)3 * QUAD_WORDS * k);
     Fp4 Aw = A;
@@ -802,7 +850,14 @@ __global__ void TBG_LAUNCH k_rlc_gident_check(DevBatch B) {
   }
   if (!lead) return;
   if (!found) {
-    push_group_chunks(B, g);
+    // a large group (many partials: 7-of-10 duties, mixed thresholds) is
+    // narrowed by chunks first rather than checked partial by partial
+    if (B.gident == 2 || m > TBG_GID_L3_MAX) {
+      push_group_chunks(B, g);
+    } else {
+      for (uint32_t d = d0; d < d1; ++d)
+        if (rlc_combinable(B, d)) rlc_push_partials(B, d);
+    }
     return;
   }
   uint32_t w = 0;
@@ -906,13 +961,14 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
   if (B.rlc_group != 0) {
     uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
+    // level-0 and level-1 Miller products on hexads by default (two waves per
+    // SIMD, k_miller_hex.hip); TBG_L0_HEX=0 runs the trio forms
+    static const bool hex = [] {
+      const char* e = getenv("TBG_L0_HEX");
+      return !e || atoi(e) != 0;
+    }();
     if (B.rlc_batch) {
       // level 0: the P chunks (kept for the group levels) and S, one product
-      // (on hexads by default: two waves per SIMD; TBG_L0_HEX=0 runs the trio form)
-      static const bool hex = [] {
-        const char* e = getenv("TBG_L0_HEX");
-        return !e || atoi(e) != 0;
-      }();
       if (hex)
         launch_l0_miller_hex(B, st);
       else
@@ -935,6 +991,8 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
       TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
       launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
       TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_GROUP_S>, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
+    } else if (hex) {
+      launch_groups_miller_hex(B, st);
     } else {
       TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_GROUPS>, grid_for(fp12_threads(n_groups * (nch + 1))), dim3(kBlock), st, B);
     }
@@ -942,9 +1000,12 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
       // level 1g before the chunks: its unresolved groups add to the chunk list
-      TBG_KLAUNCH(k_rlc_gident_lines, grid_for(n_groups), dim3(kBlock), st, B);
+      uint32_t W = 1;
+      while (W < B.rlc_group) W <<= 1;
+      TBG_KLAUNCH(k_rlc_gident_lines, grid_for(n_groups * W), dim3(kBlock), st, B);
       fb_passes(B, n_groups, [&](const DevBatch& P, uint32_t n) {
         launch_lines_fold(P, FOLD_GID, n, st);
+        TBG_KLAUNCH(k_rlc_gident_miller, grid_for(fp12_threads(n * (nch + 1))), dim3(kBlock), st, P);
         TBG_KLAUNCH(k_rlc_gident_check, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
       });
       TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);

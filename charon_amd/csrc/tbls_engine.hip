@@ -560,6 +560,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_gfe = sec(G > 1 ? 4ull * 3 * 4 * NL * ng : 0);
   size_t w_gidl = sec(G > 1 ? 4ull * ng : 0);
   size_t w_gidp = sec(G > 1 ? sizeof(G1A) * (size_t)ng * G : 0);
+  size_t w_gidf = sec(G > 1 ? 4ull * 3 * 4 * NL * ng * (nch + 1) : 0);
   size_t w_idl = sec(G > 1 ? 4ull * nd : 0);
   size_t w_idp = sec(G > 1 ? sizeof(G1A) * (size_t)nd : 0);
   size_t w_mr = sec(l0 ? 8ull * np : 0);
@@ -728,15 +729,16 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.cid_list = (uint32_t*)(dw + w_cidl);
   B.cid_p = (G1A*)(dw + w_cidp);
   B.cid_lines = B.sig_lines;
-  static const uint32_t gident = [] {  // A/B knob: TBG_GIDENT=0 sends failed groups straight to level 1.5
-    const char* e = getenv("TBG_GIDENT");
-    return e ? (uint32_t)(atoi(e) != 0) : 1u;
+  static const uint32_t gident = [] {  // A/B knob: TBG_GIDENT=0 sends failed groups straight to level 1.5;
+    const char* e = getenv("TBG_GIDENT");   // 2: level 1g, then its unresolved groups' chunks to level 1.5
+    return e ? (uint32_t)atoi(e) : 1u;
   }();
-  B.gident = G > 1 ? gident : 0u;
+  B.gident = G > 1 && G <= 64 ? gident : 0u;  // (level 1g's lines kernel runs a lane per duty of a group)
   B.grp_fe = (uint32_t*)(dw + w_gfe);
   B.gid_list = (uint32_t*)(dw + w_gidl);
   B.gid_p = (G1A*)(dw + w_gidp);
   B.gid_lines = B.sig_lines;
+  B.gid_f = (uint32_t*)(dw + w_gidf);
   B.id_list = (uint32_t*)(dw + w_idl);
   B.id_p = (G1A*)(dw + w_idp);
   B.id_lines = B.sig_lines;

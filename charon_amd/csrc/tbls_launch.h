@@ -85,11 +85,13 @@ struct DevBatch {
   uint32_t* cid_lines;    // [fb window][LINES_WORDS] lines of sum w_d S_d, by level-1.5b position - fb_base
   // level 1g: the exponent test over a failed GROUP's partials, right after
   // level 1 (most failed groups hold exactly one bad partial)
-  uint32_t gident;        // 1: failed groups go to level 1g first (0: straight to level 1.5)
+  uint32_t gident;        // 1: failed groups go to level 1g first, its unresolved ones to level 3
+                          // (2: to level 1.5; 0: no level 1g)
   uint32_t* grp_fe;       // [n_groups][3][4 NL] final-exponentiated value A_g of a level-1g group (by list position)
   uint32_t* gid_list;     // [n_groups] level-1g entries: group index (| ID_DEGENERATE)
-  G1A* gid_p;             // [n_groups][rlc_group] sum_(i in d) w_i r_i pk_i as (-x, y), by level-1g position
+  G1A* gid_p;             // [n_groups][rlc_group] sum_(i in d) w_i r_i pk_i as (-x, y): level-1g position, duty in group
   uint32_t* gid_lines;    // lines of sum w_i r_i sig_i by level-1g position - fb_base (the fallback line buffer)
+  uint32_t* gid_f;        // [n_groups][chunks + 1][3][4 NL] Miller products of a level-1g entry (chunks, then S')
   uint32_t* id_fe;        // [n_duties][3][4 NL] value A_d of each level-2b duty (by list position)
   uint32_t* id_list;      // [n_duties] level-2b entries: failed duties with several candidates
   G1A* id_p;              // [n_duties] sum w_i r_i pk_i (affine), by level-2b position
@@ -223,6 +225,8 @@ void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_s
 void launch_l0_check(const DevBatch& B, hipStream_t st);
 // level 0's P-chunk and S Miller products on hexads (k_miller_hex.hip)
 void launch_l0_miller_hex(const DevBatch& B, hipStream_t st);
+// level 1's P-chunk and group-S Miller products on hexads (k_miller_hex.hip)
+void launch_groups_miller_hex(const DevBatch& B, hipStream_t st);
 // pk_tab: the keys' pair tables (k_pubkey_tables); unused after a level-0 failure (level 0 formed the G1 products)
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);
