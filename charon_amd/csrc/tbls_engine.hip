@@ -130,7 +130,10 @@ static int grow_pinned(uint8_t** p, size_t* cap, size_t need) {
   if (*cap >= need) return TBG_OK;
   if (*p) hipHostFree(*p);
   *p = nullptr;
-  size_t n = align_up(need + need / 4, 1 << 20);
+  // 25 % headroom for small arenas; big ones (a 16 x 10k-DV slot's work
+  // arena is ~5.9 GB, 3.7 GB of it the H(m) Miller lines) round up to 256 MiB
+  // instead, so a slot's HBM stays ~ its layout while batch sizes jitter
+  const size_t n = need < (1ull << 30) ? align_up(need + need / 4, 1 << 20) : align_up(need, 1ull << 28);
   if (hipHostMalloc((void**)p, n, hipHostMallocDefault) != hipSuccess) { *cap = 0; return TBG_E_OOM; }
   *cap = n;
   return TBG_OK;
@@ -140,7 +143,10 @@ static int grow_device(uint8_t** p, size_t* cap, size_t need) {
   if (*cap >= need) return TBG_OK;
   if (*p) hipFree(*p);
   *p = nullptr;
-  size_t n = align_up(need + need / 4, 1 << 20);
+  // 25 % headroom for small arenas; big ones (a 16 x 10k-DV slot's work
+  // arena is ~5.9 GB, 3.7 GB of it the H(m) Miller lines) round up to 256 MiB
+  // instead, so a slot's HBM stays ~ its layout while batch sizes jitter
+  const size_t n = need < (1ull << 30) ? align_up(need + need / 4, 1 << 20) : align_up(need, 1ull << 28);
   if (hipMalloc((void**)p, n) != hipSuccess) { *cap = 0; return TBG_E_OOM; }
   *cap = n;
   return TBG_OK;

@@ -33,9 +33,24 @@ def host_cores():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         avail = machine
+    quota = cgroup_cpus()
+    if quota:
+        avail = min(avail, quota)
     share = os.environ.get("OMP_NUM_THREADS")
     n = min(avail, int(share)) if share and share.isdigit() and int(share) > 0 else avail
     return max(1, n), machine
+
+
+def cgroup_cpus():
+    """CPUs the cgroup's CFS quota allows (cgroup v2 cpu.max), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q == "max":
+            return None
+        return max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
 
 
 def run_cpu_baseline(batch, seconds: float = 15.0, chunk: int = 512):
@@ -68,7 +83,9 @@ def run_cpu_baseline(batch, seconds: float = 15.0, chunk: int = 512):
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 3), "unit": "DV-duties/s", "cores": cores, "kind": "port",
             "per_core": round(done / dt / cores, 3), "machine_cores": machine,
+            "cgroup_cpus": cgroup_cpus(),
             "sample": f"first {done} DVs of the rank-0 bench batch ({batch.t}-of-{n}); C restatement of the "
-                      f"reference per-item schedule (oracle/c), {cores} threads = this job's core share "
-                      f"(OMP_NUM_THREADS; the machine has {machine}), {dt:.1f}s; not the Go reference",
+                      f"reference per-item schedule (oracle/c), {cores} threads = every core this job may use "
+                      f"(affinity, cgroup quota, OMP_NUM_THREADS; the machine has {machine}), {dt:.1f}s; "
+                      f"not the Go reference",
             "mismatches": mismatches}
