@@ -735,10 +735,14 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.cid_list = (uint32_t*)(dw + w_cidl);
   B.cid_p = (G1A*)(dw + w_cidp);
   B.cid_lines = B.sig_lines;
-  static const uint32_t gident = [] {  // A/B knob: TBG_GIDENT=0 sends failed groups straight to level 1.5;
-    const char* e = getenv("TBG_GIDENT");   // 2: level 1g, then its unresolved groups' chunks to level 1.5
-    return e ? (uint32_t)atoi(e) : 1u;
-  }();
+  // Level 1g is opt-in: TBG_GIDENT=1 (unresolved groups
+  // to level 3) or 2 (to level 1.5), read per submit.  Measured
+  // (profiles/r03/gident/): +7 % at 1 % invalid in 20-step runs, whose three
+  // launches reach their latency-bound fallback levels together, but -3 % at
+  // 48 steps and -11 % on config 5, where launches overlap and the
+  // narrowing's shorter lists matter more than its extra levels.
+  const char* gid_env = getenv("TBG_GIDENT");
+  const uint32_t gident = gid_env ? (uint32_t)atoi(gid_env) : 0u;
   B.gident = G > 1 && G <= 64 ? gident : 0u;  // (level 1g's lines kernel runs a lane per duty of a group)
   B.grp_fe = (uint32_t*)(dw + w_gfe);
   B.gid_list = (uint32_t*)(dw + w_gidl);
