@@ -82,51 +82,21 @@ __device__ void agg_emit(const DevBatch& B, uint32_t d, const G2J& acc) {
   B.duty_status[d] = TBG_DS_OK;
 }
 
-// Integer-mode combination for duties of at most 32 partials, inline: the
-// participants as a bitmask, sum_j N_j P_j by double-and-add over the few
-// bits of |N_j| (3-of-4: 2 bits) with the point bodies in the kernel's own
-// code -- no out-of-line tss_combine call and no 256-byte mask on the stack.
-template <bool SPEC>
-__device__ __forceinline__ G2J combine_int_small(const DevBatch& B, uint32_t first, uint32_t n, uint32_t pmask,
-                                                 uint64_t& D) {
-  int nbits = 0;
-  for (uint32_t j = 0; j < n; ++j) {
-    if (!((pmask >> j) & 1u)) continue;
-    const uint32_t* w = B.lam + 8ull * (first + j);
-    const int b = bitlen_u64((uint64_t)w[0] | ((uint64_t)w[1] << 32));
-    nbits = nbits > b ? nbits : b;
-  }
-  G2J acc = jac_inf<Fp2>();
-  for (int bit = nbits - 1; bit >= 0; --bit) {
-    acc = jac_dbl_in(acc);
-    for (uint32_t j = 0; j < n; ++j) {
-      if (!((pmask >> j) & 1u)) continue;
-      const uint32_t* w = B.lam + 8ull * (first + j);
-      const uint64_t mag = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-      if (!((mag >> bit) & 1)) continue;
-      G2A p = B.sig_aff[first + j];
-      if (w[7] & 1) p.y = fp2_reduce(fp2_neg(p.y));
-      acc = jac_add_aff_in(acc, p);
-    }
-  }
-  const uint32_t* w0 = B.lam + 8ull * (first + (uint32_t)__builtin_ctz(pmask));
-  D = (uint64_t)w0[2] | ((uint64_t)w0[3] << 32);
-  return acc;
-}
+constexpr uint32_t AGG_EXC = 0x80000000u;  // agg_list flag: the [1/D] ladder met the doubling case
+constexpr uint32_t AGG_REF = 0x40000000u;  // agg_list flag: the whole combination on the reference path
 
-// Duties whose participants' integer Lagrange coefficients share a
-// denominator D > 1 (a partial missing from the middle of the id range,
-// e.g. ids {1,2,4}: lambda_1 = 8/3) need a 255-bit [1/D] multiplication.
-// Inline, one such duty makes its whole 64-lane wave pay that loop; they are
-// listed here instead and finished by k_aggregate_finish in uniform waves.
-// The affine conversion of the finished sums is batched over the workgroup
-// (bls_batchinv.h): every thread reaches it, with or without a sum to emit.
+// A duty's aggregation status before any curve work (kryptology's checks in
+// CombineSignatures' order; reference tbls/tss.go:142-149, :181): TBG_DS_OK
+// when a combination is due.  Lane `writer` zeroes the output first.
+// pmask: the participants among the first 32 partials; fast: the integer
+// coefficient form of at most 32 partials (combine_int_pair) applies.
 template <bool SPEC>
-__device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& emit) {
-  emit = false;
-  agg_store_zero(B, d);
-  uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
-  uint32_t n = last - first;
+__device__ int32_t agg_status(const DevBatch& B, uint32_t d, bool writer, uint32_t& pmask, bool& fast) {
+  pmask = 0;
+  fast = false;
+  if (writer) agg_store_zero(B, d);
+  const uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
+  const uint32_t n = last - first;
   if (B.op == TBG_OP_VERIFY) return TBG_DS_NOT_AGGREGATED;
   int k = 0;
   bool decode_err = false, identity = false;
@@ -153,50 +123,117 @@ __device__ int32_t agg_prepare(const DevBatch& B, uint32_t d, G2J& acc, bool& em
         return TBG_DS_AGG_DUPLICATE_ID;
     }
   }
-  uint64_t D = 1;
-  uint32_t pmask = 0;
   for (uint32_t j = first; j < last && j - first < 32; ++j)
     if (participates<SPEC>(B.op, B.partial_status[j])) pmask |= 1u << (j - first);
-  if (n <= 32 && (B.lam[8ull * (first + (uint32_t)__builtin_ctz(pmask)) + 7] & LAM_INT_FLAG)) {
-    acc = combine_int_small<SPEC>(B, first, n, pmask, D);
-  } else {  // mod-r coefficients or more than 32 partials: the general form
-    uint8_t mask[256];
-    for (uint32_t j = first; j < last; ++j) mask[j - first] = participates<SPEC>(B.op, B.partial_status[j]) ? 1 : 0;
-    acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
-  }
-  if (D > 1) {
-    B.agg_acc[d] = acc;
-    B.agg_list[atomicAdd(&B.counters[CNT_AGG], 1u)] = d;
-    return TBG_DS_OK;  // (k_aggregate_finish emits it)
-  }
-  emit = true;
+  fast = n <= 32 && (B.lam[8ull * (first + (uint32_t)__builtin_ctz(pmask)) + 7] & LAM_INT_FLAG);
   return TBG_DS_OK;
 }
 
+// The integer-form combination sum_j N_j P_j on a lane pair (bls_pair.h: one
+// Fp2 component per lane): double-and-add over the few bits of |N_j|
+// (3-of-4: 2 bits) with the branch-free group law; a doubling case sets exc
+// (the duty then takes the reference path).
 template <bool SPEC>
-__global__ void __launch_bounds__(BINV_BLOCK) k_aggregate(DevBatch B) {
-  if (spec_skip(B, SPEC)) return;  // (grid-uniform)
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = d < B.n_duties;
-  G2J acc = jac_inf<Fp2>();
-  bool emit = false;
-  int32_t st = in ? agg_prepare<SPEC>(B, d, acc, emit) : TBG_DS_OK;
-  G2A a;
-  const bool aff = block_jac_to_aff<BINV_WAVES>(acc, emit, a);  // every thread of the workgroup
-  if (!in) return;
-  if (!emit) {
-    if (st != TBG_DS_OK) B.duty_status[d] = st;  // listed D > 1 duties: k_aggregate_finish sets it
-    return;
+__device__ __forceinline__ Jac<Fp2x> combine_int_pair(const DevBatch& B, uint32_t first, uint32_t n, uint32_t pmask,
+                                                     uint64_t& D, bool& exc) {
+  int nbits = 0;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (!((pmask >> j) & 1u)) continue;
+    const uint32_t* w = B.lam + 8ull * (first + j);
+    const int b = bitlen_u64((uint64_t)w[0] | ((uint64_t)w[1] << 32));
+    nbits = nbits > b ? nbits : b;
   }
-  if (!aff) {
-    B.duty_status[d] = TBG_DS_AGG_IDENTITY;
-    return;
+  Jac<Fp2x> acc = jac_inf<Fp2x>();
+  for (int bit = nbits - 1; bit >= 0; --bit) {
+    acc = jac_dbl_lo(acc);
+    for (uint32_t j = 0; j < n; ++j) {
+      if (!((pmask >> j) & 1u)) continue;
+      const uint32_t* w = B.lam + 8ull * (first + j);
+      const uint64_t mag = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      if (!((mag >> bit) & 1)) continue;
+      Aff<Fp2x> p = px_load(B.sig_aff[first + j]);
+      if (w[7] & 1) p.y = f_reduce(f_neg(p.y));
+      acc = jac_add_aff_x(acc, p, exc);
+    }
   }
-  agg_store_compressed(B, d, a);
-  B.duty_status[d] = TBG_DS_OK;
+  const uint32_t* w0 = B.lam + 8ull * (first + (uint32_t)__builtin_ctz(pmask));
+  D = (uint64_t)w0[2] | ((uint64_t)w0[3] << 32);
+  return acc;
 }
 
-constexpr uint32_t AGG_EXC = 0x80000000u;  // agg_list flag: finish on the reference path
+// The reference form of one duty's aggregation (single lane, any coefficient
+// form, [1/D] inline): for the duties the pair kernels hand over.
+template <bool SPEC>
+__device__ void agg_reference(const DevBatch& B, uint32_t d) {
+  uint32_t pmask;
+  bool fast;
+  const int32_t st = agg_status<SPEC>(B, d, true, pmask, fast);
+  if (st != TBG_DS_OK) {
+    B.duty_status[d] = st;
+    return;
+  }
+  const uint32_t first = B.duty_first[d], n = B.duty_first[d + 1] - first;
+  uint8_t mask[256];
+  for (uint32_t j = 0; j < n; ++j) mask[j] = participates<SPEC>(B.op, B.partial_status[first + j]) ? 1 : 0;
+  uint64_t D = 1;
+  G2J acc = tss_combine(B.sig_aff + first, B.lam + 8ull * first, mask, (int)n, &D);
+  if (D > 1) acc = tss_div_den(acc, D);
+  agg_emit(B, d, acc);
+}
+
+// One lane PAIR per duty: the status checks, the integer-form combination in
+// pair form (two waves per SIMD; the single-lane kernel held 766 registers at
+// one wave), then the affine conversion with the Fp norms' inversion batched
+// over the workgroup and the 96-byte compression.  D > 1 sums go to
+// k_aggregate_finish; other coefficient forms and doubling cases to the
+// reference path (k_aggregate_exc).
+template <bool SPEC>
+__global__ void __launch_bounds__(BINV_BLOCK, TBG_PAIR_WAVES) k_aggregate(DevBatch B) {
+  if (spec_skip(B, SPEC)) return;  // (grid-uniform)
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, d = t >> 1;
+  const bool lead = pair_par() == 0;
+  const bool in = d < B.n_duties;
+  uint32_t pmask = 0;
+  bool fast = false;
+  const int32_t st = in ? agg_status<SPEC>(B, d, lead, pmask, fast) : TBG_DS_OK;
+  bool want = in && st == TBG_DS_OK;
+  if (want && !fast) {
+    if (lead) B.agg_list[atomicAdd(&B.counters[CNT_AGG], 1u)] = d | AGG_REF;
+    want = false;
+  }
+  Jac<Fp2x> acc = jac_inf<Fp2x>();
+  if (want) {
+    uint64_t D = 1;
+    bool exc = false;
+    const uint32_t first = B.duty_first[d];
+    acc = combine_int_pair<SPEC>(B, first, B.duty_first[d + 1] - first, pmask, D, exc);
+    if (exc || D > 1) {
+      if (!exc) px_store(B.agg_acc[d], acc);
+      if (lead) B.agg_list[atomicAdd(&B.counters[CNT_AGG], 1u)] = exc ? (d | AGG_REF) : d;
+      want = false;
+    }
+  }
+  const bool present = want && !jac_is_inf(acc);
+  const Fp Zp = pair_xch(acc.Z.v);
+  const Fp ni = block_batch_inv<BINV_WAVES>(fp_mul2(acc.Z.v, acc.Z.v, Zp, Zp), present);  // every thread
+  if (!in) return;
+  if (st != TBG_DS_OK) {
+    if (lead) B.duty_status[d] = st;
+    return;
+  }
+  if (!want) return;  // k_aggregate_finish / k_aggregate_exc set it
+  if (!present) {
+    if (lead) B.duty_status[d] = TBG_DS_AGG_IDENTITY;
+    return;
+  }
+  const Fp2x zi = f_mulfp(px_conj(acc.Z), ni);  // 1 / Z = conj(Z) / N(Z)
+  const Fp2x zi2 = f_sqr(zi);
+  const G2A a = {px_gather(f_mul(acc.X, zi2)), px_gather(f_mul(acc.Y, f_mul(zi2, zi)))};
+  if (lead) {
+    agg_store_compressed(B, d, a);
+    B.duty_status[d] = TBG_DS_OK;
+  }
+}
 
 // this lane's component of the same pair-form point on lane ^ m
 __device__ __forceinline__ Jac<Fp2x> shfl_xor_px(const Jac<Fp2x>& a, int m) {
@@ -219,7 +256,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_aggregate_finish(DevBatch B) {
   const uint32_t k = t >> 3;
   const int q = (int)((t >> 1) & 3);
   if (spec_skip(B, SPEC)) return;
-  if (k >= B.counters[CNT_AGG]) return;  // 8-lane uniform
+  if (k >= B.counters[CNT_AGG] || (B.agg_list[k] & AGG_REF)) return;  // 8-lane uniform
   const uint32_t d = B.agg_list[k];
   uint32_t first = B.duty_first[d], last = B.duty_first[d + 1];
   uint32_t j = first;
@@ -256,8 +293,14 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_aggregate_finish(DevBatch B) {
 template <bool SPEC>
 __global__ void TBG_LAUNCH k_aggregate_exc(DevBatch B) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (spec_skip(B, SPEC) || k >= B.counters[CNT_AGG] || !(B.agg_list[k] & AGG_EXC)) return;
-  const uint32_t d = B.agg_list[k] & ~AGG_EXC;
+  if (spec_skip(B, SPEC) || k >= B.counters[CNT_AGG]) return;
+  const uint32_t entry = B.agg_list[k];
+  if (entry & AGG_REF) {
+    agg_reference<SPEC>(B, entry & ~AGG_REF);
+    return;
+  }
+  if (!(entry & AGG_EXC)) return;
+  const uint32_t d = entry & ~AGG_EXC;
   uint32_t j = B.duty_first[d];
   while (j < B.duty_first[d + 1] && !participates<SPEC>(B.op, B.partial_status[j])) ++j;
   const uint32_t* w = B.lam + 8ull * j;
@@ -271,7 +314,7 @@ void launch_lagrange(const DevBatch& B, hipStream_t st, bool spec) {
 }
 void launch_aggregate(const DevBatch& B, hipStream_t st, bool spec) {
   if (!B.n_duties) return;
-  const dim3 grid((B.n_duties + BINV_BLOCK - 1) / BINV_BLOCK);
+  const dim3 grid((2 * B.n_duties + BINV_BLOCK - 1) / BINV_BLOCK);  // a lane pair per duty
   if (spec) TBG_KLAUNCH(k_aggregate<true>, grid, dim3(BINV_BLOCK), st, B);
   else TBG_KLAUNCH(k_aggregate<false>, grid, dim3(BINV_BLOCK), st, B);
 }
