@@ -45,26 +45,47 @@ TBG_HD Fp wide_mul_c(int c, const Fp2& x, const Fp2& y) {
   return c == 0 ? fp_mul2(x.c0, y.c0, x.c1, fp_neg(y.c1)) : fp_mul2(x.c0, y.c1, x.c1, y.c0);
 }
 
-// ---- cyclotomic squaring: products (lanes 0..11), then combination (lanes 0..2)
+// Per-lane choices are per-limb selects (fp_select), never ternaries on
+// structs: those compile to selects of addresses and put their operands in
+// scratch memory.
+TBG_HD Fp2 wide_sel2(bool k, const Fp2& x, const Fp2& y) { return {fp_select(k, x.c0, y.c0), fp_select(k, x.c1, y.c1)}; }
+// component j (0, 1) of xi u from u's two components (lazy: < u + 16p)
+TBG_HD Fp wide_xi_c(int j, const Fp& u0, const Fp& u1) { return fp_select(j == 0, fp_sub(u0, u1), fp_add(u0, u1)); }
+
+// ---- cyclotomic squaring: products (lanes 0..11), then combination (lanes
+// 0..11, one output component each: lane 4 q + k writes component k of A_q)
 TBG_HD void wide_cyc_products(int lane, const Fp* A, Fp* R) {
   if (lane >= 12) return;
   const int q = lane >> 2, k = (lane >> 1) & 1, c = lane & 1;
   const Fp2 a = wide_fp2(A, 4 * q), b = wide_fp2(A, 4 * q + 2);
   // fp4_sqr's two products: ab, (a + b)(a + xi b)
-  const Fp2 x = k == 0 ? a : fp2_add(a, b);
-  const Fp2 y = k == 0 ? b : fp2_add(a, fp2_mul_xi(b));
+  const Fp2 x = wide_sel2(k == 0, a, fp2_add(a, b));
+  const Fp2 y = wide_sel2(k == 0, b, fp2_add(a, fp2_mul_xi(b)));
   R[lane] = wide_mul_c(c, x, y);
 }
+// quad_cyc_lane(q, A_q, T_x), T_x = fp4_sqr(A_x) = {s - (ab + xi ab), 2 ab},
+// component k:  s1 = q == 1 ? xi T.b : T.a,  s2 = q == 1 ? T.a : T.b,
+//   a = 3 s1 -+ 2 A.a (q == 1: +),  b = 3 s2 +- 2 A.b (q == 1: -)
 TBG_HD void wide_cyc_combine(int lane, Fp* A, const Fp* R) {
-  if (lane >= 3) return;
-  const int q = lane, x = WIDE_SW12[q];
-  const Fp2 ab = wide_fp2(R, 4 * x), s = wide_fp2(R, 4 * x + 2);
-  const Fp2 u = fp2_reduce(fp2_add(ab, fp2_mul_xi(ab)));
-  const Fp4 T = {fp2_reduce(fp2_sub(s, u)), fp2_reduce(fp2_add(ab, ab))};  // fp4_sqr(A_x)
-  wide_put4(A, q, quad_cyc_lane(q, wide_fp4(A, q), T));
+  if (lane >= 12) return;
+  const int q = lane >> 2, k = lane & 3, x = WIDE_SW12[q], j = k & 1;
+  const Fp ab0 = R[4 * x], ab1 = R[4 * x + 1];
+  const Fp abj = fp_select(j == 0, ab0, ab1);
+  const Fp sj = R[4 * x + 2 + j];
+  const Fp Taj = fp_reduce(fp_sub(sj, fp_reduce(fp_add(abj, wide_xi_c(j, ab0, ab1)))));  // T.a component j
+  const Fp Tb0 = fp_reduce(fp_add(ab0, ab0)), Tb1 = fp_reduce(fp_add(ab1, ab1));
+  const Fp Tbj = fp_select(j == 0, Tb0, Tb1);
+  const Fp xTbj = fp_reduce(wide_xi_c(j, Tb0, Tb1));
+  // s: a components (k < 2) take s1, b components s2
+  const Fp sv = k < 2 ? fp_select(q == 1, xTbj, Taj) : fp_select(q == 1, Taj, Tbj);
+  const Fp own = A[4 * q + k];
+  const bool plus = (k < 2) == (q == 1);  // a: + on q == 1; b: + on q != 1
+  const Fp s3 = fp_mul_small(sv, 3), a2 = fp_add(own, own);
+  A[4 * q + k] = fp_reduce(fp_select(plus, fp_add(s3, a2), fp_sub(s3, a2)));
 }
 
-// ---- product C = X Y: products (lanes 0..35), then combination (lanes 0..2)
+// ---- product C = X Y: products (lanes 0..35), then combination (lanes
+// 0..11, one output component each)
 TBG_HD void wide_mul_products(int lane, const Fp* X, const Fp* Y, Fp* R) {
   if (lane >= WIDE_PROD) return;
   const int m = lane / 6, k = (lane % 6) >> 1, c = lane & 1;
@@ -78,20 +99,46 @@ TBG_HD void wide_mul_products(int lane, const Fp* X, const Fp* Y, Fp* R) {
     y = fp4_add(wide_fp4(Y, n1), wide_fp4(Y, n2));
   }
   // fp4_mul's three Fp2 products: a a', b b', (a + b)(a' + b')
-  const Fp2 u = k == 0 ? x.a : k == 1 ? x.b : fp2_add(x.a, x.b);
-  const Fp2 v = k == 0 ? y.a : k == 1 ? y.b : fp2_add(y.a, y.b);
+  const Fp2 u = wide_sel2(k == 0, x.a, wide_sel2(k == 1, x.b, fp2_add(x.a, x.b)));
+  const Fp2 v = wide_sel2(k == 0, y.a, wide_sel2(k == 1, y.b, fp2_add(y.a, y.b)));
   R[lane] = wide_mul_c(c, u, v);
 }
 TBG_HD Fp4 wide_fp4_from_products(const Fp* R, int m) {
   const Fp2 t0 = wide_fp2(R, 6 * m), t1 = wide_fp2(R, 6 * m + 2), s = wide_fp2(R, 6 * m + 4);
   return {fp2_reduce(fp2_add(t0, fp2_mul_xi(t1))), fp2_reduce(fp2_sub(s, fp2_add(t0, t1)))};
 }
+// component i (0..3: a.c0, a.c1, b.c0, b.c1) of product m = fp4 from R
+TBG_HD Fp wide_pc(const Fp* R, int m, int i) {
+  const int j = i & 1;
+  const Fp t0 = R[6 * m + j], t1 = R[6 * m + 2 + j];
+  const Fp a = fp_add(t0, wide_xi_c(j, R[6 * m + 2], R[6 * m + 3]));
+  const Fp b = fp_sub(R[6 * m + 4 + j], fp_add(t0, t1));
+  return fp_reduce(fp_select(i < 2, a, b));
+}
+// quad_combine(q, P, Pn, Pp, Qx), component k:
+//   T = Qx - (f1 + f2), f1 = q == 1 ? Pp : Pn, f2 = q == 0 ? Pp : P
+//   q = 0: (xi T.b + P.a, T.a + P.b);  q = 1: (T.a + xi Pn.b, T.b + Pn.a);  q = 2: T + Pp
 TBG_HD void wide_mul_combine(int lane, Fp* C, const Fp* R) {
-  if (lane >= 3) return;
-  const int q = lane;
-  const Fp4 P = wide_fp4_from_products(R, q), Pn = wide_fp4_from_products(R, (q + 1) % 3),
-            Pp = wide_fp4_from_products(R, (q + 2) % 3), Qx = wide_fp4_from_products(R, 3 + WIDE_SW12[q]);
-  wide_put4(C, q, quad_combine(q, P, Pn, Pp, Qx));
+  if (lane >= 12) return;
+  const int q = lane >> 2, k = lane & 3, j = k & 1;
+  const int mP = q, mn = (q + 1) % 3, mp = (q + 2) % 3, mQ = 3 + WIDE_SW12[q];
+  const int m1 = q == 1 ? mp : mn, m2 = q == 0 ? mp : mP;
+  auto Tc = [&](int i) { return fp_reduce(fp_sub(wide_pc(R, mQ, i), fp_add(wide_pc(R, m1, i), wide_pc(R, m2, i)))); };
+  Fp v;
+  if (k < 2) {
+    // the xi term: of T.b (q = 0) or Pn.b (q = 1); q = 2 has none
+    const Fp u0 = q == 0 ? Tc(2) : wide_pc(R, mn, 2), u1 = q == 0 ? Tc(3) : wide_pc(R, mn, 3);
+    const Fp xu = fp_reduce(wide_xi_c(j, u0, u1));
+    const Fp t = Tc(k);
+    const Fp w = q == 2 ? wide_pc(R, mp, k) : wide_pc(R, mP, k);
+    v = fp_select(q == 0, fp_add(xu, w), fp_select(q == 1, fp_add(t, xu), fp_add(t, w)));
+  } else {
+    // q = 0: T.a_j + P.b_j;  q = 1: T.b_j + Pn.a_j;  q = 2: T.b_j + Pp.b_j
+    const Fp t = Tc(q == 0 ? j : k);
+    const Fp w = wide_pc(R, q == 0 ? mP : (q == 1 ? mn : mp), q == 1 ? j : k);
+    v = fp_add(t, w);
+  }
+  C[4 * q + k] = fp_reduce(v);
 }
 
 // ---- the cheap per-coefficient maps (lanes 0..2) and the inversion (lane 0)

@@ -31,6 +31,7 @@ void hc_fp_sqr(const uint8_t* a, uint8_t* out) { to_be(fp_sqr(from_be(a)), out);
 void hc_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { to_be(fp_add(from_be(a), from_be(b)), out); }
 void hc_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { to_be(fp_sub(from_be(a), from_be(b)), out); }
 void hc_fp_inv(const uint8_t* a, uint8_t* out) { to_be(fp_inv(from_be(a)), out); }
+void hc_fp_inv_fermat(const uint8_t* a, uint8_t* out) { to_be(fp_inv_fermat(from_be(a)), out); }
 
 // Fp2 multiply: inputs (c0, c1) each 48 bytes
 void hc_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {

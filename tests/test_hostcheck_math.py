@@ -49,6 +49,7 @@ def test_fp_ops():
     for a in vals[1:10]:
         if a % P:
             assert fe(call("hc_fp_inv", be(a))) == pow(a, P - 2, P)
+            assert fe(call("hc_fp_inv_fermat", be(a))) == pow(a, P - 2, P)
 
 
 def f2b(x):
