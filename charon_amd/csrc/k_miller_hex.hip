@@ -21,6 +21,10 @@ namespace tbg {
 #ifndef TBG_HEX_WAVES
 #define TBG_HEX_WAVES 2
 #endif
+#ifndef TBG_HEX_HOIST
+#define TBG_HEX_HOIST 1
+#endif
+constexpr uint32_t HEX_HOIST_MAX = 16;
 
 // One hexad per (group, chunk of rlc_chunk duties), then the S hexads, as
 // k_rlc_miller_chunks (k_rlc.hip):
@@ -60,6 +64,26 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_miller_hex(DevBatch B) {
   }
   Fp4h f = hex_one();
   int idx = 0;
+#if TBG_HEX_HOIST
+  // The chunk's duties are decided once, not at every one of the 68 steps:
+  // a bit per duty whose line products run (combined, H(m) usable) and its
+  // message index in LDS, so a step's line loads do not wait behind the
+  // dv_state -> duty_msg -> h_status load chain.  Chunks longer than
+  // HEX_HOIST_MAX duties keep the per-step test.
+  __shared__ uint32_t s_msg[kBlock * HEX_HOIST_MAX];
+  uint32_t* my_msg = s_msg + HEX_HOIST_MAX * threadIdx.x;
+  const bool hoist = d1 - d0 <= HEX_HOIST_MAX;
+  uint32_t run = 0;
+  if (hoist) {
+    for (uint32_t d = d0; d < d1; ++d) {
+      if (B.dv_state[d] != RLC_COMBINED) continue;
+      const uint32_t m = B.duty_msg[d];
+      if (B.h_status[m] != 0) continue;  // the check fails in k_l0_fold / k_rlc_group_final
+      my_msg[d - d0] = m;
+      run |= 1u << (d - d0);
+    }
+  }
+#endif
 #pragma unroll 1
   for (int b = 62; b >= 0; --b) {
     if (b != 62) f = hex_sqr(f);
@@ -67,6 +91,17 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_miller_hex(DevBatch B) {
 #pragma unroll 1
     for (int s = 0; s < steps; ++s, ++idx) {
       if (s_quad) f = hex_line_folded(f, ls, idx);
+#if TBG_HEX_HOIST
+      if (hoist) {
+#pragma unroll 1
+        for (uint32_t bits = run; bits; bits &= bits - 1) {
+          const uint32_t j = __builtin_ctz(bits);
+          const G1A& P = B.dv_p[d0 + j];
+          f = hex_line_at(f, B.h_lines + (size_t)LINES_WORDS * my_msg[j], idx, fp_reduce(fp_neg(P.x)), P.y);
+        }
+        continue;
+      }
+#endif
 #pragma unroll 1
       for (uint32_t d = d0; d < d1; ++d) {
         if (B.dv_state[d] != RLC_COMBINED) continue;
