@@ -26,7 +26,16 @@
 
 namespace tbg {
 
-constexpr int BINV_WAVES = 4;                 // waves per workgroup of the batched kernels
+// One wave per workgroup by default: with three launches in flight, a
+// workgroup of four waves needs four free SIMD slots on one CU at once and
+// waits behind the other launches' one-wave workgroups (a 0.7 ms
+// k_hash_affine took 30 ms inside a 20-step run, rocprof trace in
+// profiles/r03/final4/); one-wave groups invert 4x as often but start at
+// once: 2.18-2.21 M vs 2.12-2.16 M DV-duties/s (profiles/r03/prio/).
+#ifndef TBG_BINV_WAVES
+#define TBG_BINV_WAVES 1
+#endif
+constexpr int BINV_WAVES = TBG_BINV_WAVES;    // waves per workgroup of the batched kernels
 constexpr int BINV_BLOCK = 64 * BINV_WAVES;   // their workgroup size
 
 #if defined(__HIP__)  // (device code; declared in both passes of a .hip unit)

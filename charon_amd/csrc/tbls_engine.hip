@@ -223,9 +223,22 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // per slot also overlap a batch's hash_to_G2 with its decode (lower
   // single-batch latency when queues are plentiful).
   const bool two = cfg && cfg->streams_per_slot >= 2;
-  for (auto& s : c->slots) {
-    if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
-        (two && hipStreamCreateWithFlags(&s.st2, hipStreamNonBlocking) != hipSuccess)) {
+  // TBG_SLOT_PRIO (A/B knob, read at init): 1 = slot k's streams at priority
+  // least - k (later slots ahead of earlier ones in the workgroup dispatcher),
+  // 2 = the reverse, unset / 0 = the default priority for every slot.
+  const char* prio_env = getenv("TBG_SLOT_PRIO");
+  const int prio_mode = prio_env ? atoi(prio_env) : 0;
+  int least = 0, greatest = 0;
+  if (prio_mode) hipDeviceGetStreamPriorityRange(&least, &greatest);
+  for (size_t k = 0; k < c->slots.size(); ++k) {
+    auto& s = c->slots[k];
+    const int step = prio_mode == 1 ? (int)k : (int)(c->slots.size() - 1 - k);
+    const int prio = std::max(greatest, least - step);
+    auto mk = [&](hipStream_t* st) {
+      return prio_mode ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio)
+                       : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    };
+    if (mk(&s.st) != hipSuccess || (two && mk(&s.st2) != hipSuccess)) {
       tbg_destroy(c);
       return TBG_E_DEVICE;
     }
