@@ -291,7 +291,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_aggregate_finish(DevBatch B) {
 // The listed duties whose pair-form ladder met the doubling case: the
 // single-lane reference form (one thread per list entry).
 template <bool SPEC>
-__global__ void TBG_LAUNCH k_aggregate_exc(DevBatch B) {
+__global__ void TBG_LAUNCH_N(2) k_aggregate_exc(DevBatch B) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (spec_skip(B, SPEC) || k >= B.counters[CNT_AGG]) return;
   const uint32_t entry = B.agg_list[k];

@@ -309,7 +309,7 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
 // ------------------------------------------------------------------ level 0
 // One quad per group: the product of its P-chunk values (k_rlc_miller_chunks,
 // MILLER_L0); a combined duty whose H(m) is unusable makes level 0 fail.
-__global__ void TBG_LAUNCH k_l0_fold(DevBatch B) {
+__global__ void TBG_LAUNCH_N(2) k_l0_fold(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk;
   const uint32_t n_groups = (B.n_duties + G - 1) / G, nch = (G + C - 1) / C, nq = nch + 1;
@@ -324,18 +324,18 @@ __global__ void TBG_LAUNCH k_l0_fold(DevBatch B) {
   }
   const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nq * g;
   Fp4 f = quad_load(base);
-  for (uint32_t c = 1; c < nch; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
+  for (uint32_t c = 1; c < nch; ++c) f = quad_mul_in(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
   quad_store(B.grp_f + (size_t)3 * QUAD_WORDS * g, f);
 }
 
 // Product tree, one quad per L0_TREE_FAN values of grp_f[in .. in + n).
-__global__ void TBG_LAUNCH k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32_t out) {
+__global__ void TBG_LAUNCH_N(2) k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32_t out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t q = fp12_slot(t), a0 = q * L0_TREE_FAN;
   if (a0 >= n || B.counters[CNT_L0_BAD]) return;
   const uint32_t a1 = min(a0 + L0_TREE_FAN, n);
   Fp4 f = quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a0));
-  for (uint32_t a = a0 + 1; a < a1; ++a) f = quad_mul(f, quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
+  for (uint32_t a = a0 + 1; a < a1; ++a) f = quad_mul_in(f, quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
   quad_store(B.grp_f + (size_t)3 * QUAD_WORDS * (out + q), f);
 }
 
