@@ -120,8 +120,7 @@ STAGE_KERNELS = {
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
                 "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>"],
     "h_lines": ["k_lines_h"],
-    "verify": ["k_miller_hex<MILLER_L0>", "k_miller_hex<MILLER_GROUPS>", "k_rlc_miller_chunks<MILLER_L0>", "k_rlc_miller_chunks<MILLER_GROUP_S>",
-               "k_rlc_miller_chunks<MILLER_GROUPS>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after",
+    "verify": ["k_miller_hex<MILLER_L0>", "k_miller_hex<MILLER_GROUPS>", "k_miller_hex<MILLER_GROUP_S>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after",
                "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_gident_lines", "k_lines_fold<FOLD_GID>",
                "k_rlc_gident_miller", "k_rlc_gident_check", "k_rlc_chunk_lines", "k_lines_fold<FOLD_CHUNKS>",
                "k_rlc_check_chunks", "k_rlc_cident_lines", "k_lines_fold<FOLD_CID>", "k_rlc_cident_check",
@@ -136,10 +135,24 @@ STAGE_KERNELS = {
 ROCPROF_NAME = {
     "k_miller_hex<MILLER_L0>": "void tbg::k_miller_hex<1>(tbg::DevBatch)",
     "k_miller_hex<MILLER_GROUPS>": "void tbg::k_miller_hex<0>(tbg::DevBatch)",
-    "k_rlc_miller_chunks<MILLER_L0>": "void tbg::k_rlc_miller_chunks<1>(tbg::DevBatch)",
-    "k_rlc_miller_chunks<MILLER_GROUP_S>": "void tbg::k_rlc_miller_chunks<2>(tbg::DevBatch)",
-    "k_rlc_miller_chunks<MILLER_GROUPS>": "void tbg::k_rlc_miller_chunks<0>(tbg::DevBatch)",
+    "k_miller_hex<MILLER_GROUP_S>": "void tbg::k_miller_hex<2>(tbg::DevBatch)",
 }
+# one Fp product of the engine's 14 x 28-bit limbs = 392 u32 mul-adds (196 for
+# the product, 196 for the REDC); SURVEY.md 8(d) prices one at 300 (12 x 32-bit
+# CIOS): frac_fp300 states the same measured Fp-product rate on that basis
+MADS_PER_FP_MUL = 392
+SURVEY_MADS_PER_FP_MUL = 300
+
+
+def rocprof_name(k):
+    """The symbol rocprofv3 prints for a launch-site name."""
+    return ROCPROF_NAME.get(k, "tbg::" + k + "(...)")
+
+
+def traffic_key(k):
+    """The key tools/pmc_traffic.py files a kernel under: rocprofv3's symbol
+    without 'void tbg::' and the argument list (k_miller_hex<1>, k_lagrange<true>)."""
+    return rocprof_name(k).split("(")[0].replace("void ", "").replace("tbg::", "")
 
 
 def kernel_profile(prof):
@@ -177,15 +190,19 @@ def kernel_roofline(wm, kp, items, tm, batches):
     mads = m["mads"] * items[m["per"]] + m.get("plus_per_launch", 0)
     ms, launches = kp[k]
     ach = mads / (ms * 1e-3) / 1e12
-    short = k.split("<")[0]
     traffic = None
-    if tm and short in tm.get("kernels", {}):
-        kk = tm["kernels"][short]
+    kk = (tm or {}).get("kernels", {}).get(traffic_key(k))
+    if kk:
         traffic = int(1024 * (2 * kk.get("FETCH_SIZE_KB_per_launch", 0) + kk.get("WRITE_SIZE_KB_per_launch", 0))
                       * batches / max(1, tm.get("batches_per_launch", 1)))
-    return {"bound": "valu-int-mul", "kernel": k, "rocprof_name": ROCPROF_NAME.get(k, "tbg::" + k + "(...)"),
+    fp_mul_per_s = ach * 1e12 / MADS_PER_FP_MUL
+    return {"bound": "valu-int-mul", "kernel": k, "rocprof_name": rocprof_name(k),
             "achieved": round(ach, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
-            "frac": round(ach / PEAK_MAD_TOPS, 4), "traffic": traffic,
+            "frac": round(ach / PEAK_MAD_TOPS, 4),
+            "frac_fp300": round(fp_mul_per_s * SURVEY_MADS_PER_FP_MUL / 1e12 / PEAK_MAD_TOPS, 4),
+            "fp_mul_per_s": round(fp_mul_per_s, 1),
+            "traffic": traffic, "traffic_unit": "bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
+                                                "profiles/traffic_latest.json)" if traffic is not None else None,
             "algorithmic_mads_per_launch": int(mads), "work_model": f"{m['mads']} mads per {m['per']}"
             + (f" + {m['plus_per_launch']} per launch" if m.get("plus_per_launch") else ""),
             "items_per_launch": items[m["per"]], "launch_ms": round(ms / launches, 4),
@@ -287,6 +304,69 @@ def batch_exact(res, b, eng):
     return bool(np.array_equal(res.agg[ok], b.group_sig[ok]))
 
 
+def config4_multi(args):
+    """BASELINE config 4 through the one-process multi-device product path:
+    the 1M-DV 3-of-4 batch (1 % invalid partials of every kind when
+    --inject > 0) as `--multi-batches` caller batches handed to
+    tbg_multi_submit_group, cut over `--multi-contexts` contexts (one per
+    visible GPU, or several per GPU when fewer GPUs are visible -- on a
+    one-GPU box eight contexts share it), gathered into caller order by
+    tbg_multi_collect.  Host packing, H2D, the chains and D2H are all inside
+    the clock (the product path, not HBM-resident); every result is checked."""
+    import torch
+    from charon_amd import engine as eng
+    from tools.workload import make_mixed_batch
+    from charon_amd.shard import sub_batch
+    ndev = max(1, torch.cuda.device_count())
+    devs = [i % ndev for i in range(args.multi_contexts)]
+    m = eng.MultiEngine(devs, slots=1)
+    try:
+        t0 = time.perf_counter()
+        b = make_mixed_batch(m.context(0), args.dvs, seed=args.seed, inject=args.inject, thresholds=((3, 4),),
+                             load=m.load_pubkeys)
+        gen_s = time.perf_counter() - t0
+        K = max(1, args.multi_batches)
+        cuts = [args.dvs * k // K for k in range(K + 1)]
+        calls, subs = [], []
+        for k in range(K):
+            sb = sub_batch(cuts[k], cuts[k + 1], b.duty_first, b.sigs, b.identifiers, pubkey_ids=b.pubkey_ids,
+                           duty_threshold=b.threshold, msg_data=b.msg_data, msg_off=b.msg_off, duty_msg=b.duty_msg)
+            subs.append(sb)
+            calls.append(dict(duty_first=sb.duty_first, sigs=sb.sigs, identifiers=sb.identifiers,
+                              msgs=(sb.msg_data, sb.msg_off), duty_msg=sb.duty_msg, pubkey_ids=sb.pubkey_ids,
+                              duty_threshold=sb.duty_threshold))
+
+        def one_round():
+            ts = m.submit_group(eng.OP_VERIFY_AGGREGATE, calls)
+            return [m.collect(t) for t in ts]
+
+        res = one_round()  # untimed: the first round allocates every context's arenas
+        rounds = max(1, args.steps)
+        t0 = time.perf_counter()
+        for _ in range(rounds):
+            res = one_round()
+        dt = time.perf_counter() - t0
+        ps = np.concatenate([r.partial_status for r in res])
+        ds = np.concatenate([r.duty_status for r in res])
+        agg = np.concatenate([r.agg for r in res])
+        ok = ds == eng.DS_OK
+        exact = bool(np.array_equal(ps == eng.PS_VALID, ~b.injected) and np.array_equal(ok, b.expect_ok)
+                     and np.array_equal(agg[ok], b.group_sig[ok]))
+        return {"metric": METRIC, "value": round(args.dvs * rounds / dt, 2),
+                "unit": "DV-duties/s (n verifies + 1 aggregate each)", "n_gpus": ndev, "steps": rounds,
+                "warmup": 1, "ms_per_step": round(dt * 1e3 / rounds, 3), "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "u32 (Fp 14x28-bit limbs)",
+                "data": f"synthetic (seeded, generated on the GPU), {args.inject:.2%} injected invalid partials",
+                "config": {"workload": f"config4 via tbg_multi: {args.dvs}-DV 3-of-4 batch as {K} caller batches, "
+                                       f"cut over {len(devs)} contexts on {ndev} GPU(s)",
+                           "contexts": len(devs), "caller_batches": K,
+                           "path": "tbg_multi_submit_group + tbg_multi_collect (host packing, PCIe, chains, "
+                                   "gather); one step = the whole batch"},
+                "exact": exact, "generation_s": round(gen_s, 1)}
+    finally:
+        m.close()
+
+
 WORKLOADS = {
     "config2": "config2: 3-of-4, {dvs} DVs x 1 attestation per GPU",
     "config3": "config3: 7-of-10, {dvs} DVs x 1 attestation per GPU",
@@ -325,10 +405,23 @@ def main():
                     help="config2: 10k 3-of-4 DVs per step (the headline); config3: 100k 7-of-10 DVs per step; "
                          "config4: each GPU's 125k-DV shard of the 1M-DV 3-of-4 batch; config5: 10k mixed duties "
                          "with 1%% invalid partials of every kind per step")
+    ap.add_argument("--multi-contexts", type=int, default=0,
+                    help="config4 only: run the 1M-DV batch through tbg_multi_* over this many contexts in ONE "
+                         "process (one per visible GPU, repeated when fewer are visible) instead of the "
+                         "per-rank 125k-DV shard")
+    ap.add_argument("--multi-batches", type=int, default=8,
+                    help="caller batches the 1M-DV batch is handed over as (tbg_multi_submit_group)")
     ap.add_argument("--api-batches", type=int, default=192,
                     help="batches pushed through the product path (tbg_submit / tbg_collect, host packing and PCIe "
                          "included) for the api_pipeline side key; 0 skips it")
     args = ap.parse_args()
+    if args.workload == "config4" and args.multi_contexts:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            sys.exit("bench.py: --multi-contexts drives every GPU from one process (no torch.distributed launch)")
+        args.dvs = 1_000_000 if args.dvs == 10000 else args.dvs
+        args.inject = 0.0 if args.inject is None else args.inject
+        print(json.dumps(config4_multi(args)))
+        return
     if args.workload == "config4":
         args.dvs, args.t, args.n = 125000, 3, 4
         args.inflight, args.merge = min(args.inflight, 2), 1  # ~19 GB of HBM per resident 125k-DV batch

@@ -38,6 +38,12 @@ def sources():
                   if f.endswith((".h", ".hip", ".cpp"))) + HEADERS
 
 
+# What the last build() call did (reported by __graft_entry__.build): "reused"
+# (the in-tree library was newer than every source), "compiled" (units
+# recompiled with hipcc, then linked) or "relinked" (objects up to date).
+LAST_BUILD = {"mode": None}
+
+
 def is_stale():
     if not os.path.exists(LIB_PATH):
         return True
@@ -52,6 +58,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     tuning variant elsewhere (tools/ab_variants.py)."""
     target = out or LIB_PATH
     if not force and out is None and not is_stale():
+        LAST_BUILD.update(mode="reused", target=target, units_compiled=0, units_total=0)
         return LIB_PATH
     from concurrent.futures import ThreadPoolExecutor
     hipcc = _hipcc()
@@ -73,12 +80,15 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     host_flags = ["-O3", "-std=c++17", "-fPIC"] + ["-D" + d for d in defines] + \
         [f for f in extra_flags if f != "-Xarch_host"]
 
+    compiled = []
+
     def compile_unit(u):
         obj = os.path.join(objdir, os.path.splitext(u)[0] + ".o")
         if same_flags and not force and os.path.exists(obj):
             t = os.path.getmtime(obj)
             if all(os.path.getmtime(d) < t for d in headers + [os.path.join(CSRC, u)]):
                 return obj  # up to date (incremental rebuild)
+        compiled.append(u)
         if u.endswith(".cpp"):
             cmd = [_clangxx()] + host_flags + ["-c", os.path.join(CSRC, u), "-o", obj]
         else:
@@ -100,6 +110,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(target + ".tmp", target)
+    LAST_BUILD.update(mode="compiled" if compiled else "relinked", target=target, units_compiled=len(compiled),
+                      units_total=len(units))
     return target
 
 
@@ -169,6 +181,8 @@ class TbgConfig(ctypes.Structure):
         ("rlc_chunk", ctypes.c_uint32),
         ("streams_per_slot", ctypes.c_uint32),
         ("rlc_batch", ctypes.c_uint32),
+        ("gident", ctypes.c_uint32),
+        ("fb_window", ctypes.c_uint32),
     ]
 
 
@@ -212,6 +226,7 @@ SIGNATURES = {
     "tbg_multi_load_pubkeys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                               ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p]),
     "tbg_multi_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TbgBatch), ctypes.POINTER(ctypes.c_uint64)]),
+    "tbg_multi_submit_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     "tbg_multi_collect": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int]),
     "tbg_multi_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),

@@ -499,16 +499,9 @@ TBG_HD Fp fp_inv_vartime(const Fp& a) {
   return fp_mul(fp_select(li_is_one(u), x1, x2), fp_from_const(R3_L));
 }
 
-#ifndef TBG_INV_FERMAT
-#define TBG_INV_FERMAT 0  // 1: Fermat for every inversion (A/B)
-#endif
-TBG_HD Fp fp_inv(const Fp& a) {
-#if TBG_INV_FERMAT
-  return fp_inv_fermat(a);
-#else
-  return fp_inv_vartime(a);
-#endif
-}
+// The inversion of every public value (see fp_inv_vartime).  Values that
+// depend on a secret key call fp_inv_fermat directly (k_gen.hip).
+TBG_HD Fp fp_inv(const Fp& a) { return fp_inv_vartime(a); }
 
 // Big-endian bytes (48) -> integer limbs; also reports whether value < p.
 TBG_HD Fp fp_limbs_from_be48(const uint8_t* b, bool* lt_p) {

@@ -1,9 +1,8 @@
-// Level 0's P-chunk Miller products on hexads (bls_hex.h): the MILLER_L0 mode
-// of k_rlc_miller_chunks (k_rlc.hip) with each Fp12 spread over six lanes
-// instead of three, so the kernel fits 256 VGPRs and runs at two waves per
-// SIMD.  Same slots, same products, same quad-layout output (chunk_f,
-// batch_f): the level-0 fold / tree / final kernels and the group levels read
-// them unchanged.  Reference: the pairing products behind tbls.Verify
+// The level-0 and level-1 Miller products on hexads (bls_hex.h): each Fp12
+// spread over six lanes instead of a trio's three, so the kernel fits 256
+// VGPRs and runs at two waves per SIMD.  Output in the trio's quad layout
+// (chunk_f, batch_f): the level-0 fold / tree / final kernels and the group
+// levels read it with trio kernels.  Reference: the pairing products behind tbls.Verify
 // (tbls/tss.go:190-197), batched per k_rlc.hip's header.
 //
 // Products are kept in program order (TBG_SCHED_FENCE): interleaving two
@@ -26,20 +25,24 @@ namespace tbg {
 #endif
 constexpr uint32_t HEX_HOIST_MAX = 16;
 
-// One hexad per (group, chunk of rlc_chunk duties), then the S hexads, as
-// k_rlc_miller_chunks (k_rlc.hip):
-//   MILLER_L0      ONE S hexad for level 0's batch-wide S (batch lines, -g1 folded)
-//   MILLER_GROUPS  one S hexad per group (group lines); groups without
-//                  candidates skipped, a degenerate group S keeps its P chunks
+// One hexad per (group, chunk of rlc_chunk duties), then the S hexads (S
+// hexads evaluate one line per step instead of C: in waves of their own they
+// finish early instead of each holding a P chunk's wave slot):
+//   MILLER_L0       ONE S hexad for level 0's batch-wide S (batch lines, -g1 folded)
+//   MILLER_GROUPS   one S hexad per group (group lines); groups without
+//                   candidates skipped, a degenerate group S keeps its P chunks
+//   MILLER_GROUP_S  after a level-0 failure: the groups' S hexads only (level
+//                   0's P-chunk products serve the group checks as they are)
 template <int MODE>
 __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_miller_hex(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk;
   const uint32_t n_groups = (B.n_duties + G - 1) / G;
   const uint32_t nch = (G + C - 1) / C, nq = nch + 1;
-  const uint32_t np_q = n_groups * nch;
+  const uint32_t np_q = MODE == MILLER_GROUP_S ? 0u : n_groups * nch;
   const uint32_t qd = hex_slot(t);
   if (qd == 0xFFFFFFFFu || qd >= np_q + (MODE == MILLER_L0 ? 1u : n_groups)) return;
+  if (MODE == MILLER_GROUP_S && B.counters[CNT_L0_OK]) return;  // level 0 accepted the batch
   const bool s_quad = qd >= np_q;
   const uint32_t* ls = nullptr;
   uint32_t* dst;
@@ -50,7 +53,7 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_miller_hex(DevBatch B) {
     dst = B.batch_f;
   } else {
     const uint32_t g = s_quad ? qd - np_q : qd / nch, c = s_quad ? nch : qd % nch;
-    if (MODE == MILLER_GROUPS) {
+    if (MODE != MILLER_L0) {
       const int32_t gs = B.grp_state[g];
       if (gs == GRP_EMPTY || (gs == GRP_FAIL && s_quad)) return;
     }
@@ -124,6 +127,10 @@ void launch_groups_miller_hex(const DevBatch& B, hipStream_t st) {
   const uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
   const uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
   TBG_KLAUNCH(k_miller_hex<MILLER_GROUPS>, grid_for(hex_threads(n_groups * (nch + 1))), dim3(kBlock), st, B);
+}
+void launch_group_s_miller_hex(const DevBatch& B, hipStream_t st) {
+  const uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
+  TBG_KLAUNCH(k_miller_hex<MILLER_GROUP_S>, grid_for(hex_threads(n_groups)), dim3(kBlock), st, B);
 }
 
 }  // namespace tbg

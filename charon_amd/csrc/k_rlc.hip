@@ -185,83 +185,12 @@ __device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
   return A;
 }
 
-// Level 1, Miller part: one quad per (group, chunk of rlc_chunk duties),
-// plus one quad per group for the group's S pair alone (chunk index nch).
+// Level 1, Miller part: one hexad per (group, chunk of rlc_chunk duties),
+// plus one per group for the group's S pair alone (k_miller_hex.hip).
 // Chunks share nothing but the final exponentiation, so a group's pairs are
-// spread over several quads -- and because the P pairs of a chunk are kept
+// spread over several hexads -- and because the P pairs of a chunk are kept
 // apart from S, a failed group can re-check its chunks (level 1.5) from these
 // same products with only S_c's Miller loop added.
-//   MILLER_GROUPS   P chunks, then every group's S quad (no level 0);
-//   MILLER_L0       P chunks, then ONE quad for level 0's S (batch_f);
-//   MILLER_GROUP_S  after a level-0 failure: the groups' S quads only (the P
-//                   chunk products of level 0 serve the group checks as they are).
-// (a template on the mode: each mode is its own kernel symbol, so per-kernel
-// profiles separate level 0's P chunks from the fallback-only S quads)
-template <int MODE>
-__global__ void TBG_LAUNCH_N(TBG_CHUNK_WAVES) k_rlc_miller_chunks(DevBatch B) {
-  constexpr int mode = MODE;
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t G = B.rlc_group, C = B.rlc_chunk;
-  uint32_t n_groups = (B.n_duties + G - 1) / G;
-  uint32_t nch = (G + C - 1) / C, nq = nch + 1;
-  // P chunks first, then the S quads: S quads evaluate one line per step
-  // instead of C, and in waves of their own they finish early instead of
-  // each holding a P chunk's wave slot for its full length
-  uint32_t qd = fp12_slot(t);
-  const uint32_t np_q = n_groups * nch;
-  uint32_t g, c;
-  bool l0_s = false;
-  if (mode == MILLER_GROUP_S) {
-    if (B.counters[CNT_L0_OK] || qd >= n_groups) return;
-    g = qd;
-    c = nch;
-  } else {
-    if (qd >= (mode == MILLER_L0 ? np_q + 1 : n_groups * nq)) return;
-    l0_s = mode == MILLER_L0 && qd == np_q;
-    g = qd < np_q ? qd / nch : qd - np_q;
-    c = qd < np_q ? qd % nch : nch;
-  }
-  const uint32_t* ls;
-  uint32_t* dst;
-  uint32_t d0 = 0, d1 = 0;
-  if (l0_s) {
-    if (B.counters[CNT_L0_BAD]) return;
-    ls = B.batch_lines;
-    dst = B.batch_f;
-  } else {
-    qd = g * nq + c;  // storage index
-    // a group whose S sum degenerated (GRP_FAIL here) still gets its P-chunk
-    // products: level 1.5 re-checks its chunks from them.  (Level 0's P
-    // chunks run before any group state exists.)
-    if (mode != MILLER_L0) {
-      const int32_t gs = B.grp_state[g];
-      if (gs == GRP_EMPTY || (gs == GRP_FAIL && c == nch)) return;
-    }
-    uint32_t gd1 = min(g * G + G, B.n_duties);
-    d0 = g * G + c * C;
-    d1 = c == nch ? d0 : min(d0 + C, gd1);
-    ls = B.grp_lines + (size_t)LINES_WORDS * g;
-    dst = B.chunk_f + (size_t)3 * QUAD_WORDS * qd;
-  }
-  const bool s_quad = l0_s || c == nch;
-  Fp4 f = quad_one();
-  int idx = 0;
-  for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = quad_sqr_in(f);
-    int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-    for (int s = 0; s < steps; ++s, ++idx) {
-      if (s_quad) f = quad_line_folded<true>(f, ls, idx);
-      for (uint32_t d = d0; d < d1; ++d) {
-        if (B.dv_state[d] != RLC_COMBINED) continue;
-        uint32_t m = B.duty_msg[d];
-        if (B.h_status[m] != 0) continue;  // the group fails in k_rlc_group_final
-        const G1A& P = B.dv_p[d];
-        f = quad_line_at<true>(f, B.h_lines + (size_t)LINES_WORDS * m, idx, fp_reduce(fp_neg(P.x)), P.y);
-      }
-    }
-  }
-  quad_store(dst, f);
-}
 
 // Level 1, final part: one quad per group multiplies its chunks' products
 // (the S chunk included) and runs the one final exponentiation of the group.
@@ -961,18 +890,11 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
   if (B.rlc_group != 0) {
     uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
     uint32_t nch = (B.rlc_group + B.rlc_chunk - 1) / B.rlc_chunk;
-    // level-0 and level-1 Miller products on hexads by default (two waves per
-    // SIMD, k_miller_hex.hip); TBG_L0_HEX=0 runs the trio forms
-    static const bool hex = [] {
-      const char* e = getenv("TBG_L0_HEX");
-      return !e || atoi(e) != 0;
-    }();
+    // the level-0 and level-1 Miller products run on hexads (two waves per
+    // SIMD, k_miller_hex.hip; the trio form measured 16.2 vs 15.2 ms, round 3)
     if (B.rlc_batch) {
       // level 0: the P chunks (kept for the group levels) and S, one product
-      if (hex)
-        launch_l0_miller_hex(B, st);
-      else
-        TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_L0>, grid_for(fp12_threads((n_groups * nch + 1))), dim3(kBlock), st, B);
+      launch_l0_miller_hex(B, st);
       TBG_KLAUNCH(k_l0_fold, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
       uint32_t in = 0, n = n_groups, out = n_groups;
       while (n > L0_TREE_FAN) {
@@ -990,11 +912,9 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
       TBG_KLAUNCH(k_rlc_duty_sum<DSUM_FALLBACK_S>, duty_grid(B), dim3(BINV_BLOCK), st, B);
       TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
       launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
-      TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_GROUP_S>, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
-    } else if (hex) {
-      launch_groups_miller_hex(B, st);
+      launch_group_s_miller_hex(B, st);
     } else {
-      TBG_KLAUNCH(k_rlc_miller_chunks<MILLER_GROUPS>, grid_for(fp12_threads(n_groups * (nch + 1))), dim3(kBlock), st, B);
+      launch_groups_miller_hex(B, st);
     }
     TBG_KLAUNCH(k_rlc_group_final, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);

@@ -37,15 +37,22 @@ struct KProfRec {
   hipEvent_t a, b;
 };
 static thread_local std::vector<KProfRec>* g_kprof = nullptr;
+// Every launch pushes a record, even when an event could not be created (its
+// null events are skipped by kprof_post and reported as failed by the
+// readout), so a record never takes a neighbour's end event.
 void kprof_pre(const char* kernel, hipStream_t st) {
   if (!g_kprof) return;
   KProfRec r{kernel, nullptr, nullptr};
-  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return;
-  (void)hipEventRecord(r.a, st);
+  if (hipEventCreate(&r.a) != hipSuccess) r.a = nullptr;
+  if (r.a && hipEventCreate(&r.b) != hipSuccess) {
+    (void)hipEventDestroy(r.a);
+    r.a = r.b = nullptr;
+  }
+  if (r.a) (void)hipEventRecord(r.a, st);
   g_kprof->push_back(r);
 }
 void kprof_post(hipStream_t st) {
-  if (!g_kprof || g_kprof->empty()) return;
+  if (!g_kprof || g_kprof->empty() || !g_kprof->back().b) return;
   (void)hipEventRecord(g_kprof->back().b, st);
 }
 }  // namespace tbg
@@ -118,6 +125,8 @@ struct tbg_ctx {
   double invalid_ema = 0.0;  // exponential average of the invalid share of collected verified partials
   uint64_t rlc_seed = 0;   // 0 = OS randomness per batch
   uint64_t seed_ctr = 0;
+  uint32_t gident = TBG_GIDENT_OFF;  // level 1g routing (tbg_config.gident)
+  uint32_t fb_window = TBG_FB_WINDOW;  // fallback line buffer positions per pass (tbg_config.fb_window)
 };
 
 #define HIP_TRY(x)                       \
@@ -126,14 +135,19 @@ struct tbg_ctx {
     if (e_ != hipSuccess) return TBG_E_DEVICE; \
   } while (0)
 
+// Capacity for an arena of `need` bytes: 25 % headroom for small arenas; big
+// ones (a 16 x 10k-DV slot's work arena is ~5.9 GB) get 1/16 headroom rounded
+// up to 256 MiB, so batch sizes that jitter around a boundary do not hipFree
+// + hipMalloc (a device-wide synchronisation) on every submit.
+static size_t arena_size(size_t need) {
+  return need < (1ull << 30) ? align_up(need + need / 4, 1 << 20) : align_up(need + need / 16, 1ull << 28);
+}
+
 static int grow_pinned(uint8_t** p, size_t* cap, size_t need) {
   if (*cap >= need) return TBG_OK;
   if (*p) hipHostFree(*p);
   *p = nullptr;
-  // 25 % headroom for small arenas; big ones (a 16 x 10k-DV slot's work
-  // arena is ~5.9 GB, 3.7 GB of it the H(m) Miller lines) round up to 256 MiB
-  // instead, so a slot's HBM stays ~ its layout while batch sizes jitter
-  const size_t n = need < (1ull << 30) ? align_up(need + need / 4, 1 << 20) : align_up(need, 1ull << 28);
+  const size_t n = arena_size(need);
   if (hipHostMalloc((void**)p, n, hipHostMallocDefault) != hipSuccess) { *cap = 0; return TBG_E_OOM; }
   *cap = n;
   return TBG_OK;
@@ -143,10 +157,7 @@ static int grow_device(uint8_t** p, size_t* cap, size_t need) {
   if (*cap >= need) return TBG_OK;
   if (*p) hipFree(*p);
   *p = nullptr;
-  // 25 % headroom for small arenas; big ones (a 16 x 10k-DV slot's work
-  // arena is ~5.9 GB, 3.7 GB of it the H(m) Miller lines) round up to 256 MiB
-  // instead, so a slot's HBM stays ~ its layout while batch sizes jitter
-  const size_t n = need < (1ull << 30) ? align_up(need + need / 4, 1 << 20) : align_up(need, 1ull << 28);
+  const size_t n = arena_size(need);
   if (hipMalloc((void**)p, n) != hipSuccess) { *cap = 0; return TBG_E_OOM; }
   *cap = n;
   return TBG_OK;
@@ -196,6 +207,9 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   if (cfg && cfg->rlc_batch > TBG_RLC_L0_OFF) { delete c; return TBG_E_INVALID_ARG; }
   if (cfg) c->rlc_batch = cfg->rlc_batch;
   c->rlc_seed = cfg ? cfg->rlc_seed : 0;
+  if (cfg && cfg->gident > TBG_GIDENT_CHUNKS) { delete c; return TBG_E_INVALID_ARG; }
+  c->gident = cfg ? cfg->gident : (uint32_t)TBG_GIDENT_OFF;
+  if (cfg && cfg->fb_window) c->fb_window = cfg->fb_window;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->retire_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->keys_ready, hipEventDisableTiming) != hipSuccess) {
@@ -223,21 +237,10 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // per slot also overlap a batch's hash_to_G2 with its decode (lower
   // single-batch latency when queues are plentiful).
   const bool two = cfg && cfg->streams_per_slot >= 2;
-  // TBG_SLOT_PRIO (A/B knob, read at init): 1 = slot k's streams at priority
-  // least - k (later slots ahead of earlier ones in the workgroup dispatcher),
-  // 2 = the reverse, unset / 0 = the default priority for every slot.
-  const char* prio_env = getenv("TBG_SLOT_PRIO");
-  const int prio_mode = prio_env ? atoi(prio_env) : 0;
-  int least = 0, greatest = 0;
-  if (prio_mode) hipDeviceGetStreamPriorityRange(&least, &greatest);
+  // (Per-slot stream priorities were measured within noise, round 3.)
   for (size_t k = 0; k < c->slots.size(); ++k) {
     auto& s = c->slots[k];
-    const int step = prio_mode == 1 ? (int)k : (int)(c->slots.size() - 1 - k);
-    const int prio = std::max(greatest, least - step);
-    auto mk = [&](hipStream_t* st) {
-      return prio_mode ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio)
-                       : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-    };
+    auto mk = [&](hipStream_t* st) { return hipStreamCreateWithFlags(st, hipStreamNonBlocking); };
     if (mk(&s.st) != hipSuccess || (two && mk(&s.st2) != hipSuccess)) {
       tbg_destroy(c);
       return TBG_E_DEVICE;
@@ -382,16 +385,8 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   const bool verify = B.op != TBG_OP_AGGREGATE;
   const G1A* pk = (const G1A*)c->d_pk;
   // With one stream per slot the two independent chains run one after the
-  // other, the per-message chain first.  TBG_ALT_ORDER=1 runs the
-  // per-signature chain first on odd slots (to stagger the latency-bound
-  // phases of batches submitted together): measured no better.
-  static const int alt_order = [] {
-    // A/B knob (measured: no gain at 20 or 48 steps, slightly worse at 48):
-    // 1 = odd slots run the per-signature chain first
-    const char* e = getenv("TBG_ALT_ORDER");
-    return e ? atoi(e) : 0;
-  }();
-  const bool sig_first = alt_order && st2 == st && ((&sl - c->slots.data()) & 1);
+  // other, the per-message chain first (running the per-signature chain
+  // first on odd slots was measured no better, round 2).
   // Level 0 on: aggregate speculatively (every candidate valid) in the
   // middle of the chain, so the launch's tail is the verification alone; the
   // regular aggregation below returns at once after a level-0 pass.
@@ -423,10 +418,10 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   if (stage < 0 || stage == 0) {
     HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
-    if ((rc = sig_first ? sig_chain() : msg_chain()) != TBG_OK) return rc;
+    if ((rc = msg_chain()) != TBG_OK) return rc;
   }
   if (stage < 0 || stage == 1)
-    if ((rc = sig_first ? msg_chain() : sig_chain()) != TBG_OK) return rc;
+    if ((rc = sig_chain()) != TBG_OK) return rc;
   if (stage >= 0 && stage != 2) return TBG_OK;
   HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
   HIP_TRY(hipEventRecord(ev[6], st));
@@ -545,7 +540,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   // The fallback levels' lines share one buffer of fb_w list positions,
   // consumed in passes (DevBatch::fb_window): a slot no longer holds 22.8 KB
   // per partial for lists that a clean batch leaves empty.
-  const uint32_t fb_w = verify ? std::max<uint32_t>(1u, std::min<uint32_t>(TBG_FB_WINDOW, np)) : 0u;
+  const uint32_t fb_w = verify ? std::max<uint32_t>(1u, std::min<uint32_t>(c->fb_window, np)) : 0u;
   size_t w_sl = sec(4ull * LINES_WORDS * fb_w);
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
   if (c->rlc_auto)
@@ -748,15 +743,12 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.cid_list = (uint32_t*)(dw + w_cidl);
   B.cid_p = (G1A*)(dw + w_cidp);
   B.cid_lines = B.sig_lines;
-  // Level 1g is opt-in: TBG_GIDENT=1 (unresolved groups
-  // to level 3) or 2 (to level 1.5), read per submit.  Measured
+  // Level 1g is opt-in (tbg_config.gident).  Measured
   // (profiles/r03/gident/): +7 % at 1 % invalid in 20-step runs, whose three
   // launches reach their latency-bound fallback levels together, but -3 % at
   // 48 steps and -11 % on config 5, where launches overlap and the
   // narrowing's shorter lists matter more than its extra levels.
-  const char* gid_env = getenv("TBG_GIDENT");
-  const uint32_t gident = gid_env ? (uint32_t)atoi(gid_env) : 0u;
-  B.gident = G > 1 && G <= 64 ? gident : 0u;  // (level 1g's lines kernel runs a lane per duty of a group)
+  B.gident = G > 1 && G <= 64 ? c->gident : 0u;  // (level 1g's lines kernel runs a lane per duty of a group)
   B.grp_fe = (uint32_t*)(dw + w_gfe);
   B.gid_list = (uint32_t*)(dw + w_gidl);
   B.gid_p = (G1A*)(dw + w_gidp);
@@ -981,13 +973,13 @@ int tbg_replay_profile(tbg_ctx* c, tbg_ticket t, tbg_kernel_time* out, uint32_t 
   for (auto& r : rec) {
     if (rc == TBG_OK && n < max_entries) {
       float ms = 0;
-      if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) rc = TBG_E_DEVICE;
+      if (!r.a || !r.b || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) rc = TBG_E_DEVICE;
       snprintf(out[n].name, sizeof(out[n].name), "%s", r.name);
       out[n].ms = ms;
       ++n;
     }
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
+    if (r.a) hipEventDestroy(r.a);
+    if (r.b) hipEventDestroy(r.b);
   }
   for (auto& e : ev) hipEventDestroy(e);
   *n_entries = n;

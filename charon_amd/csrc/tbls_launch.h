@@ -11,8 +11,8 @@
 namespace tbg {
 
 constexpr int kBlock = 64;
-// List positions per pass of the fallback levels' shared line buffer
-// (22.8 KB each: 0.75 GB per slot).
+// Default list positions per pass of the fallback levels' shared line buffer
+// (22.8 KB each: 0.75 GB per slot; tbg_config.fb_window overrides it).
 #ifndef TBG_FB_WINDOW
 #define TBG_FB_WINDOW 32768u
 #endif
@@ -32,9 +32,6 @@ constexpr int kBlock = 64;
 #endif
 #ifndef TBG_DECODE_WAVES
 #define TBG_DECODE_WAVES 2  // k_decode_sigs (square roots only)
-#endif
-#ifndef TBG_CHUNK_WAVES
-#define TBG_CHUNK_WAVES 1   // k_rlc_miller_chunks (quad Fp12, one wave per SIMD)
 #endif
 #define TBG_LAUNCH_N(w) __launch_bounds__(64, w)
 inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
@@ -150,7 +147,7 @@ constexpr uint32_t MSM_SUM_ENTRIES = MSM_BUCKETS / MSM_SUM_FAN + MSM_BUCKETS / (
 constexpr uint32_t L0_TREE_FAN = 4;
 // (sum over the passes of ceil(n / F^k) <= n / (F - 1) + one per pass)
 TBG_HD inline uint32_t grp_f_entries(uint32_t n_groups) { return n_groups + n_groups / (L0_TREE_FAN - 1) + 40; }
-// k_rlc_miller_chunks modes
+// k_miller_hex modes
 enum MillerMode : int { MILLER_GROUPS = 0, MILLER_L0 = 1, MILLER_GROUP_S = 2 };
 // k_rlc_duty_sum phases
 enum DutySumPhase : int { DSUM_BOTH = 0, DSUM_L0_P = 1, DSUM_FALLBACK_S = 2 };
@@ -227,6 +224,8 @@ void launch_l0_check(const DevBatch& B, hipStream_t st);
 void launch_l0_miller_hex(const DevBatch& B, hipStream_t st);
 // level 1's P-chunk and group-S Miller products on hexads (k_miller_hex.hip)
 void launch_groups_miller_hex(const DevBatch& B, hipStream_t st);
+// after a level-0 failure: the groups' S Miller products only (k_miller_hex.hip)
+void launch_group_s_miller_hex(const DevBatch& B, hipStream_t st);
 // pk_tab: the keys' pair tables (k_pubkey_tables); unused after a level-0 failure (level 0 formed the G1 products)
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);

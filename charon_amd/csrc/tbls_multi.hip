@@ -2,12 +2,13 @@
 // (BASELINE config 4: 1 M DV-duties over 8 x MI355X with a host gather).
 //
 // A multi-context owns one single-device context per entry of devices[].
-// Duties are independent (no cross-device math), so a batch is
-// cut into contiguous duty ranges of about equal partial counts; every range
-// becomes a sub-batch that shares the caller's arrays by pointer offset (only
-// duty_first is rebased and the messages a range uses are re-indexed), and the
-// sub-batches are packed and submitted concurrently, one host thread per
-// context.  Collection writes each shard's statuses and aggregates straight
+// Duties are independent (no cross-device math), so a batch --
+// or a group of callers' batches taken back to back -- is cut into contiguous
+// duty ranges of about equal partial counts; every piece becomes a sub-batch
+// that shares the caller's arrays by pointer offset (only duty_first is
+// rebased and the messages a range uses are re-indexed), and each context's
+// pieces are packed into ONE device batch (tbg_submit_group) and submitted
+// concurrently, one host thread per context.  Collection writes each shard's statuses and aggregates straight
 // into the caller's arrays at the shard's offsets, so the gather is the
 // per-DV loop order of core/parsigex/parsigex.go:101-107 and
 // core/parsigdb/memory.go:96-134 -> core/sigagg/sigagg.go:53-103 by
@@ -24,15 +25,18 @@
 
 namespace {
 
+// One piece of a caller batch: its duties [d0, d1) (partials [p0, p1)),
+// submitted to context `ctx` as part `ticket` of that context's device batch.
 struct Shard {
   uint32_t ctx = 0;
   tbg_ticket ticket = 0;
   uint32_t d0 = 0, d1 = 0, p0 = 0, p1 = 0;
 };
 
+// One caller batch (one multi ticket): its pieces, at most one per context.
 struct Job {
   std::vector<Shard> shards;
-  std::vector<uint32_t> duty_lo;  // [size + 1] cut points (empty shards included)
+  std::vector<uint32_t> duty_lo;  // [size + 1] cut points in the batch's duties (empty shards included)
   bool collecting = false;
 };
 
@@ -181,54 +185,111 @@ int tbg_multi_load_pubkeys(tbg_multi* m, const uint8_t* pk48, uint32_t count, ui
 }
 
 int tbg_multi_submit(tbg_multi* m, const tbg_batch* b, tbg_ticket* ticket) {
-  if (!m || !ticket) return TBG_E_INVALID_ARG;
-  int rc = validate_split(b);
-  if (rc != TBG_OK) return rc;
-  const uint32_t n = (uint32_t)m->ctx.size(), nd = b->n_duties, np = b->n_partials;
-  // Cut points: shard i starts at the first duty whose first partial is at
-  // or past i * np / n (duties with many partials are never split); with no
-  // partials at all, duties are split evenly.
-  Job job;
-  job.duty_lo.resize(n + 1);
-  job.duty_lo[0] = 0;
-  job.duty_lo[n] = nd;
-  for (uint32_t i = 1; i < n; ++i) {
-    uint32_t d;
-    if (np) {
-      const uint32_t target = (uint32_t)((uint64_t)np * i / n);
-      d = (uint32_t)(std::lower_bound(b->duty_first, b->duty_first + nd + 1, target) - b->duty_first);
-    } else {
-      d = (uint32_t)((uint64_t)nd * i / n);
-    }
-    job.duty_lo[i] = std::max(job.duty_lo[i - 1], std::min(d, nd));
+  return tbg_multi_submit_group(m, &b, 1, ticket);
+}
+
+int tbg_multi_submit_group(tbg_multi* m, const tbg_batch* const* bs, uint32_t n_batches, tbg_ticket* tickets) {
+  if (!m || !bs || !tickets || n_batches == 0) return TBG_E_INVALID_ARG;
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    const int rc = validate_split(bs[k]);
+    if (rc != TBG_OK) return rc;
+    if (bs[k]->op != bs[0]->op) return TBG_E_INVALID_ARG;  // one kernel chain per device batch
   }
+  const uint32_t n = (uint32_t)m->ctx.size();
+  // The caller batches back to back form one sequence of duties; context i
+  // takes the duties from the first one whose first partial is at or past
+  // i * P / n (P = all partials; duties are never split, a duty with many
+  // partials stays whole), so every context gets an equal share of the
+  // partials however the callers' batches are sized.  With no partials at all
+  // the duties are split evenly.  A context's range may span several caller
+  // batches: their pieces go to it as ONE tbg_submit_group (one device batch,
+  // one launch per kernel), the way a single context packs callers' batches.
+  std::vector<uint64_t> d_base(n_batches + 1, 0), p_base(n_batches + 1, 0);
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    d_base[k + 1] = d_base[k] + bs[k]->n_duties;
+    p_base[k + 1] = p_base[k] + bs[k]->n_partials;
+  }
+  const uint64_t ND = d_base[n_batches], NP = p_base[n_batches];
+  if (ND > 0x7FFFFFFFull * n || NP > 0x7FFFFFFFull * n) return TBG_E_INVALID_ARG;
+  // global duty index of the first duty whose global first partial >= target
+  // (the first duty of batch k starts at p_base[k], its last at most at
+  // p_base[k + 1]: the search starts at the first batch that can hold one)
+  auto duty_at_partial = [&](uint64_t target) -> uint64_t {
+    uint32_t k = (uint32_t)(std::lower_bound(p_base.begin() + 1, p_base.end(), target) - (p_base.begin() + 1));
+    while (k < n_batches) {
+      const tbg_batch* b = bs[k];
+      const uint64_t local = target > p_base[k] ? target - p_base[k] : 0;
+      const uint32_t d = (uint32_t)(std::lower_bound(b->duty_first, b->duty_first + b->n_duties + 1, local) -
+                                    b->duty_first);
+      if (d < b->n_duties) return d_base[k] + d;
+      ++k;  // past this batch's last duty: the next batch's first
+    }
+    return ND;
+  };
+  std::vector<uint64_t> cut(n + 1, 0);
+  cut[n] = ND;
+  for (uint32_t i = 1; i < n; ++i) {
+    const uint64_t c = NP ? duty_at_partial(NP * i / n) : ND * i / n;
+    cut[i] = std::max(cut[i - 1], std::min(c, ND));
+  }
+  // Pieces per context: (caller batch, its duty range).
+  struct Piece { uint32_t k, d0, d1; };
+  std::vector<std::vector<Piece>> pieces(n);
+  for (uint32_t i = 0; i < n; ++i)
+    for (uint32_t k = 0; k < n_batches; ++k) {
+      const uint64_t lo = std::max(cut[i], d_base[k]), hi = std::min(cut[i + 1], d_base[k + 1]);
+      if (hi > lo) pieces[i].push_back({k, (uint32_t)(lo - d_base[k]), (uint32_t)(hi - d_base[k])});
+    }
   std::vector<uint32_t> use;
   for (uint32_t i = 0; i < n; ++i)
-    if (job.duty_lo[i + 1] > job.duty_lo[i]) use.push_back(i);
+    if (!pieces[i].empty()) use.push_back(i);
   std::vector<int> src(use.size(), TBG_OK);
-  job.shards.resize(use.size());
-  parallel_for((uint32_t)use.size(), [&](uint32_t k) {
-    const uint32_t i = use[k];
-    Shard& s = job.shards[k];
-    s.ctx = i;
-    s.d0 = job.duty_lo[i];
-    s.d1 = job.duty_lo[i + 1];
-    s.p0 = b->duty_first[s.d0];
-    s.p1 = b->duty_first[s.d1];
-    SubBatch sb;
-    sb.build(*b, s.d0, s.d1);
-    src[k] = tbg_submit(m->ctx[i], &sb.b, &s.ticket);  // copies everything it needs
+  std::vector<std::vector<tbg_ticket>> part_tickets(use.size());
+  parallel_for((uint32_t)use.size(), [&](uint32_t u) {
+    const uint32_t i = use[u];
+    std::vector<SubBatch> sb(pieces[i].size());
+    std::vector<const tbg_batch*> ptr(pieces[i].size());
+    for (size_t j = 0; j < sb.size(); ++j) {
+      sb[j].build(*bs[pieces[i][j].k], pieces[i][j].d0, pieces[i][j].d1);
+      ptr[j] = &sb[j].b;
+    }
+    part_tickets[u].resize(sb.size());
+    src[u] = tbg_submit_group(m->ctx[i], ptr.data(), (uint32_t)ptr.size(), part_tickets[u].data());  // copies
   });
-  for (size_t k = 0; k < src.size(); ++k) {
-    if (src[k] == TBG_OK) continue;
-    // undo: drain the shards that did start, then report the first error
-    for (size_t j = 0; j < src.size(); ++j)
-      if (src[j] == TBG_OK) tbg_collect(m->ctx[job.shards[j].ctx], job.shards[j].ticket, nullptr, nullptr, nullptr, 1);
-    return src[k];
+  for (size_t u = 0; u < src.size(); ++u) {
+    if (src[u] == TBG_OK) continue;
+    // undo: drain the contexts that did start, then report the first error
+    for (size_t v = 0; v < src.size(); ++v)
+      if (src[v] == TBG_OK)
+        for (tbg_ticket t : part_tickets[v]) tbg_collect(m->ctx[use[v]], t, nullptr, nullptr, nullptr, 1);
+    return src[u];
+  }
+  std::vector<Job> jobs(n_batches);
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    Job& job = jobs[k];
+    job.duty_lo.resize(n + 1);
+    for (uint32_t i = 0; i <= n; ++i)
+      job.duty_lo[i] = (uint32_t)(std::min(std::max(cut[i], d_base[k]), d_base[k + 1]) - d_base[k]);
+  }
+  for (size_t u = 0; u < use.size(); ++u) {
+    const uint32_t i = use[u];
+    for (size_t j = 0; j < pieces[i].size(); ++j) {
+      const Piece& pc = pieces[i][j];
+      Shard s;
+      s.ctx = i;
+      s.ticket = part_tickets[u][j];
+      s.d0 = pc.d0;
+      s.d1 = pc.d1;
+      s.p0 = bs[pc.k]->duty_first[pc.d0];
+      s.p1 = bs[pc.k]->duty_first[pc.d1];
+      jobs[pc.k].shards.push_back(s);
+    }
   }
   std::lock_guard<std::mutex> lk(m->mu);
-  *ticket = m->next_ticket++;
-  m->jobs.emplace(*ticket, std::move(job));
+  for (uint32_t k = 0; k < n_batches; ++k) {
+    tickets[k] = m->next_ticket++;
+    m->jobs.emplace(tickets[k], std::move(jobs[k]));
+  }
   return TBG_OK;
 }
 

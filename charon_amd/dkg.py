@@ -8,6 +8,7 @@
                            then AggregateSignatures / AggregatePublicKeys
                            (plain sums: the multi-signature of all shares)
   verify_multi_signature   dkg/dkg.go:377       VerifyMultiSignature
+  lock_verify_hashes       cluster/lock.go:117-131  the JSON lock hash == hashLock(l)
   lock_verify_signatures   cluster/lock.go:137-179  the lock's aggregate
                            signature: FastAggregateVerify over every pubshare,
                            over the hash the caller recomputed (not the JSON's)
@@ -167,6 +168,18 @@ def _lock_bytes(v) -> bytes:
     return base64.b64decode(v)
 
 
+def lock_verify_hashes(lock: dict, lock_hash: bytes) -> None:
+    """The lock-hash half of Lock.VerifyHashes (cluster/lock.go:117-131): the
+    JSON's lock_hash must equal the caller's recomputed hashLock(l)
+    ("invalid lock hash").  The definition-hash half and the SSZ walk that
+    recomputes both hashes are host work outside the BLS path."""
+    lock_hash = bytes(lock_hash)
+    if len(lock_hash) != 32:
+        raise ValueError("lock_hash must be the 32-byte hashLock(l)")
+    if _lock_bytes(lock.get("lock_hash")) != lock_hash:
+        raise DKGError("invalid lock hash")
+
+
 def lock_verify_signatures(lock: dict, lock_hash: bytes | None = None, engine=None) -> None:
     """Lock.VerifySignatures' aggregate check (cluster/lock.go:137-177) over a
     lock in its JSON form: cluster_definition.version, signature_aggregate,
@@ -177,11 +190,11 @@ def lock_verify_signatures(lock: dict, lock_hash: bytes | None = None, engine=No
     the JSON carries.  hashLock's SSZ walk of the definition and validators is
     host work outside this path, so the CALLER supplies the hash it recomputed
     as `lock_hash`; without it this raises (ValueError) instead of trusting
-    the file.  A JSON lock_hash that differs from the recomputed one fails as
-    VerifyHashes does (lock.go:117-131, "invalid lock hash").  The
-    definition's operator signatures (Definition.VerifySignatures,
-    lock.go:138-140) are ECDSA work outside the BLS path and are not checked
-    here."""
+    the file.  Like VerifySignatures this never reads the JSON's lock_hash:
+    comparing it with the recomputed hash is VerifyHashes' job
+    (lock_verify_hashes).  The definition's operator signatures
+    (Definition.VerifySignatures, lock.go:138-140) are ECDSA work outside the
+    BLS path and are not checked here."""
     version = lock.get("cluster_definition", {}).get("version", "")
     sig = _lock_bytes(lock.get("signature_aggregate"))
     if not sig:
@@ -196,9 +209,6 @@ def lock_verify_signatures(lock: dict, lock_hash: bytes | None = None, engine=No
     lock_hash = bytes(lock_hash)
     if len(lock_hash) != 32:
         raise ValueError("lock_hash must be the 32-byte hashLock(l)")
-    claimed = _lock_bytes(lock.get("lock_hash"))
-    if claimed and claimed != lock_hash:
-        raise DKGError("invalid lock hash")
     e = tbls._engine(engine)
     _, st, sst = e.sum_sigs(sig, [0, 1])  # tblsconv.SigFromBytes: decode only
     if _is_decode_error(int(sst[0])):

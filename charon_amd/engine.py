@@ -26,6 +26,7 @@ NO_PUBKEY = 0xFFFFFFFF
 TIMING_KEYS = ["decode", "hash", "combine", "h_lines", "verify", "lagrange", "aggregate", "total"]
 VERIFY_RLC, VERIFY_EACH = 0, 1
 RLC_L0_AUTO, RLC_L0_ON, RLC_L0_OFF = 0, 1, 2   # tbg_config.rlc_batch
+GIDENT_OFF, GIDENT_L3, GIDENT_CHUNKS = 0, 1, 2  # tbg_config.gident
 L0_NOT_RUN, L0_PASSED, L0_FAILED = 0, 1, 2     # tbg_fetch_level0
 E_PENDING = -6
 
@@ -71,11 +72,13 @@ class Engine:
     """One context = one GPU (HIP device ordinal)."""
 
     def __init__(self, device: int = 0, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0,
-                 rlc_seed: int = 0, rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0):
+                 rlc_seed: int = 0, rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0,
+                 gident: int = GIDENT_OFF, fb_window: int = 0):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
-                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch)
+                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch,
+                                gident=gident, fb_window=fb_window)
         h = ctypes.c_void_p()
         rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
         self._check(rc, "tbg_init")
@@ -305,11 +308,13 @@ class MultiEngine:
     (several contexts on one GPU)."""
 
     def __init__(self, devices, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0, rlc_seed: int = 0,
-                 rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0):
+                 rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0, gident: int = GIDENT_OFF,
+                 fb_window: int = 0):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=0, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
-                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch)
+                                rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch,
+                                gident=gident, fb_window=fb_window)
         devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
         h = ctypes.c_void_p()
         rc = self._lib.tbg_multi_init(ctypes.byref(cfg), _ptr(devs), len(devs), ctypes.byref(h))
@@ -338,6 +343,15 @@ class MultiEngine:
         except Exception:
             pass
 
+    def context(self, i: int) -> "Engine":
+        """Context i of the multi-context as an Engine (borrowed: closing it
+        does nothing; it lives as long as the multi-context) -- e.g. to
+        generate test vectors without opening another context."""
+        h = self._lib.tbg_multi_context(self._h, i)
+        if not h:
+            raise EngineError(f"tbg_multi_context: no context {i}")
+        return _BorrowedEngine(self._lib, h, self.devices[i])
+
     def load_pubkeys(self, pk48) -> tuple[int, np.ndarray]:
         a = _u8(pk48, 48)
         n = a.shape[0]
@@ -353,6 +367,17 @@ class MultiEngine:
         self._check(self._lib.tbg_multi_submit(self._h, ctypes.byref(b), ctypes.byref(t)), "tbg_multi_submit")
         self._keep[t.value] = (nd, np_)
         return t.value
+
+    def submit_group(self, op, batches):
+        """Several batches (dicts of submit()'s arguments) as one multi-device
+        launch (tbg_multi_submit_group): one ticket per batch."""
+        built = [self._batch(op, **b) for b in batches]
+        arr = (ctypes.POINTER(_native.TbgBatch) * len(built))(*[ctypes.pointer(b) for b, _, _, _ in built])
+        t = np.zeros(len(built), dtype=np.uint64)
+        self._check(self._lib.tbg_multi_submit_group(self._h, arr, len(built), _ptr(t)), "tbg_multi_submit_group")
+        for ticket, (_, _, nd, np_) in zip(t.tolist(), built):
+            self._keep[ticket] = (nd, np_)
+        return t.tolist()
 
     def layout(self, ticket) -> list:
         out = np.zeros(self.size + 1, dtype=np.uint32)
@@ -373,6 +398,20 @@ class MultiEngine:
 
     def run(self, op, duty_first, sigs, identifiers, **kw) -> BatchResult:
         return self.collect(self.submit(op, duty_first, sigs, identifiers, **kw))
+
+
+class _BorrowedEngine(Engine):
+    """An Engine over a context owned by a MultiEngine (tbg_multi_context)."""
+
+    def __init__(self, lib, handle, device):
+        self._lib = lib
+        self._h = ctypes.c_void_p(handle)
+        self.device = device
+        self.uid = next(_serial)
+        self._keep = {}
+
+    def close(self):
+        self._h = None  # the multi-context destroys it
 
 
 from .shard import shard_bounds  # noqa: E402,F401  (re-export)

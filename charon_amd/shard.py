@@ -30,6 +30,19 @@ def shard_bounds(duty_first, n_shards: int) -> list:
     return lo + [nd]
 
 
+def group_shard_bounds(duty_firsts, n_shards: int) -> list:
+    """tbg_multi_submit_group's cut of several batches taken back to back:
+    shard_bounds over the concatenated duties, then each batch's own cut
+    points (clamped to its duties) -- one list of n_shards + 1 per batch, what
+    tbg_multi_layout reports for that batch's ticket."""
+    dfs = [np.asarray(d, dtype=np.int64) for d in duty_firsts]
+    d_base = np.cumsum([0] + [len(d) - 1 for d in dfs])
+    p_base = np.cumsum([0] + [int(d[-1]) for d in dfs])
+    glob = np.concatenate([d[:-1] + p for d, p in zip(dfs, p_base[:-1])] + [[p_base[-1]]])
+    cut = shard_bounds(glob, n_shards)
+    return [[int(min(max(c, d_base[k]), d_base[k + 1]) - d_base[k]) for c in cut] for k in range(len(dfs))]
+
+
 @dataclass
 class SubBatch:
     """Duties [d0, d1) of a batch as a batch of its own (tbg_batch fields)."""

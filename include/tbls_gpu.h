@@ -96,7 +96,18 @@ typedef struct {
   uint32_t rlc_batch;     /* level 0, the whole device batch as ONE check (RLC mode):
                            * TBG_RLC_L0_AUTO (0) while the collected batches are clean,
                            * TBG_RLC_L0_ON always, TBG_RLC_L0_OFF never              */
+  uint32_t gident;        /* level 1g (exponent test over a failed group's partials):
+                           * TBG_GIDENT_OFF (0, default), TBG_GIDENT_L3 (unresolved
+                           * groups to the per-partial level) or TBG_GIDENT_CHUNKS
+                           * (unresolved groups to the chunk level).  Fixed at init:
+                           * the library reads no environment variables.             */
+  uint32_t fb_window;     /* list positions per pass of the fallback levels' shared
+                           * Miller-line buffer (22.8 KB of HBM each; 0 -> 32768):
+                           * longer lists run in several passes                       */
 } tbg_config;
+#define TBG_GIDENT_OFF 0
+#define TBG_GIDENT_L3 1
+#define TBG_GIDENT_CHUNKS 2
 
 /* Verification schedule.  Both give every partial the verdict of the exact
  * per-item CoreVerify: RLC checks random linear combinations of groups of
@@ -254,7 +265,12 @@ int tbg_fast_aggregate_verify(tbg_ctx* ctx, const uint32_t* pubkey_ids, const ui
 /* Test-vector / benchmark-input generation on the GPU (not on the hot path):
  * tbls.Sign / PartialSign (reference tbls/tss.go:200-217) and
  * SecretKey.GetPublicKey.  sk32: 32-byte big-endian secret scalars (< r).
- * tbg_sign signs item i with sk32[i] over message item_msg[i]. */
+ * tbg_sign signs item i with sk32[i] over message item_msg[i].
+ * TEST-ONLY: the scalar multiplication by sk is a plain double-and-add whose
+ * timing depends on the key, so these entry points are not side-channel safe
+ * and must not hold a production validator key (the Z inversions of the
+ * results use the constant-time Fermat inversion, but that alone does not
+ * make the path constant time). */
 int tbg_sk_to_pk(tbg_ctx* ctx, const uint8_t* sk32, uint32_t n, uint8_t* pk48);
 int tbg_sign(tbg_ctx* ctx, const uint8_t* sk32, uint32_t n, const uint8_t* msgs, const uint32_t* msg_off,
              uint32_t n_msgs, const uint32_t* item_msg, uint8_t* sig96);
@@ -278,9 +294,14 @@ int tbg_last_timings(const tbg_ctx* ctx, float* ms8);
  * engine is initialised from the app wiring (app/app.go:321-488).
  *
  * Public keys are replicated: tbg_multi_load_pubkeys decodes the table on
- * every device (1 M DVs x 4 shares is ~0.9 GB of HBM per GPU), so any shard
- * can reference any id and the ids are the same as for a single context.
- * cfg->device is ignored (devices[] is used).  Thread-safe. */
+ * every device (1 M DVs x 4 shares x 420 B ~ 1.7 GB, 0.6 % of a GPU's 288
+ * GB), so any shard can reference any id and the ids are the same as for a
+ * single context.  Replication is the chosen design: the cut follows the
+ * partial counts of whatever batches arrive (a burst of one committee's
+ * duties still spreads over every GPU), where key-owned shards would route
+ * each duty to its keys' GPU and leave the others idle for a skewed burst
+ * (DESIGN.md section 5).  cfg->device is ignored (devices[] is used).
+ * Thread-safe. */
 typedef struct tbg_multi tbg_multi;
 int tbg_multi_init(const tbg_config* cfg, const int32_t* devices, uint32_t n_devices, tbg_multi** out);
 void tbg_multi_destroy(tbg_multi* m);
@@ -289,6 +310,14 @@ uint32_t tbg_multi_size(const tbg_multi* m);
 tbg_ctx* tbg_multi_context(tbg_multi* m, uint32_t i);
 int tbg_multi_load_pubkeys(tbg_multi* m, const uint8_t* pk48, uint32_t count, uint32_t* first_id, int32_t* status);
 int tbg_multi_submit(tbg_multi* m, const tbg_batch* batch, tbg_ticket* ticket);
+/* Several caller batches (same op) as ONE multi-device launch: the batches
+ * taken back to back are cut into n contiguous ranges of about equal partial
+ * counts, and each context's pieces are packed into one device batch
+ * (tbg_submit_group), so concurrent callers' batches fill every GPU together
+ * instead of each batch being cut into n small launches.  tickets[k] names
+ * batch k for tbg_multi_collect / tbg_multi_layout (its cut points in its own
+ * duties).  tbg_multi_submit(b) is tbg_multi_submit_group(&b, 1). */
+int tbg_multi_submit_group(tbg_multi* m, const tbg_batch* const* batches, uint32_t n_batches, tbg_ticket* tickets);
 /* Same contract as tbg_collect; block = 0 returns TBG_E_PENDING until EVERY
  * shard has finished (nothing is consumed before that). */
 int tbg_multi_collect(tbg_multi* m, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status,

@@ -63,22 +63,30 @@ def test_roofline_fields_from_work_model():
     b = types.SimpleNamespace(n_dv=10000, identifiers=np.zeros(40000), msg_off=np.zeros(10001))
     items = bench.launch_items([b] * 16, 16)
     assert items == {"partial": 640000, "message": 160000, "duty": 160000, "group": 10000, "launch": 1}
-    prof = [("k_decode_sigs", 9.0), ("k_subgroup_sigs", 13.4), ("k_rlc_miller_chunks<MILLER_L0>", 15.9),
-            ("k_rlc_miller_chunks<MILLER_GROUP_S>", 0.005), ("k_msm_sum", 0.4), ("k_msm_sum", 0.1)]
+    prof = [("k_decode_sigs", 9.0), ("k_subgroup_sigs", 13.4), ("k_miller_hex<MILLER_L0>", 15.9),
+            ("k_miller_hex<MILLER_GROUP_S>", 0.005), ("k_msm_sum", 0.4), ("k_msm_sum", 0.1)]
     kp = bench.kernel_profile(prof)
     assert kp["k_msm_sum"] == (0.5, 2)
-    r = bench.kernel_roofline(wm, kp, items, None, 16)
-    m = wm["kernels"]["k_rlc_miller_chunks<MILLER_L0>"]
+    # the PMC model files kernels under rocprofv3's symbol (k_miller_hex<1>):
+    # the dominant kernel's traffic is found by that key and scaled per launch
+    tm = {"batches_per_launch": 16, "kernels": {"k_miller_hex<1>": {"FETCH_SIZE_KB_per_launch": 100.0,
+                                                                     "WRITE_SIZE_KB_per_launch": 10.0}}}
+    r = bench.kernel_roofline(wm, kp, items, tm, 16)
+    m = wm["kernels"]["k_miller_hex<MILLER_L0>"]
     mads = m["mads"] * 10000 + m["plus_per_launch"]
-    assert r["kernel"] == "k_rlc_miller_chunks<MILLER_L0>" == r["dominant_by_exclusive_time"]
-    assert r["rocprof_name"] == "void tbg::k_rlc_miller_chunks<1>(tbg::DevBatch)"
+    assert r["kernel"] == "k_miller_hex<MILLER_L0>" == r["dominant_by_exclusive_time"]
+    assert r["rocprof_name"] == "void tbg::k_miller_hex<1>(tbg::DevBatch)"
+    assert r["traffic"] == 1024 * 210
+    assert abs(r["frac_fp300"] - r["frac"] * 300 / 392) < 1e-3
+    assert bench.traffic_key("k_lagrange<true>") == "k_lagrange<true>"
+    assert bench.traffic_key("k_miller_hex<MILLER_GROUP_S>") == "k_miller_hex<2>"
     assert r["algorithmic_mads_per_launch"] == mads
     assert abs(r["achieved"] - mads / 15.9e-3 / 1e12) < 1e-2
     assert abs(r["frac"] - r["achieved"] / bench.PEAK_MAD_TOPS) < 1e-3
     # an unpriced dominant kernel falls to the longest priced one, and says so
     kp2 = dict(kp, k_mystery=(99.0, 1))
     r2 = bench.kernel_roofline(wm, kp2, items, None, 16)
-    assert r2["dominant_by_exclusive_time"] == "k_mystery" and r2["kernel"] == "k_rlc_miller_chunks<MILLER_L0>"
+    assert r2["dominant_by_exclusive_time"] == "k_mystery" and r2["kernel"] == "k_miller_hex<MILLER_L0>"
     pipe = bench.pipeline_roofline(wm, 1.0e6, True, 3, 4)
     assert abs(pipe["achieved"] - 1.0e6 * wm["mads"]["unit_3of4_l0"] / 1e12) < 1e-2
     assert 0 < pipe["frac"] < 1

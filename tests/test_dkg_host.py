@@ -31,8 +31,12 @@ def test_lock_verify_needs_a_recomputed_hash():
             "signature_aggregate": "0x" + (b"\x80" + bytes(95)).hex()}
     with pytest.raises(ValueError, match="recomputed hashLock"):
         dkg.lock_verify_signatures(lock)
+    # the JSON hash is VerifyHashes' concern (lock.go:117-131), not VerifySignatures'
     with pytest.raises(dkg.DKGError, match="^invalid lock hash$"):
-        dkg.lock_verify_signatures(lock, b"\x01" * 32)
+        dkg.lock_verify_hashes(lock, b"\x01" * 32)
+    assert dkg.lock_verify_hashes(lock, bytes(32)) is None
+    with pytest.raises(dkg.DKGError, match="^invalid lock hash$"):
+        dkg.lock_verify_hashes({k: v for k, v in lock.items() if k != "lock_hash"}, bytes(32))
 
 
 def test_lock_byte_fields_decode_both_encodings():

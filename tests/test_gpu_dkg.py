@@ -113,15 +113,16 @@ def test_lock_verify_signatures(engine):
     # the aggregate is checked over the caller's recomputed hash, never the JSON's
     with pytest.raises(ValueError, match="recomputed hashLock"):
         dkg.lock_verify_signatures(lock, None, engine)
-    edited = dict(lock, lock_hash="0x" + bytes(32).hex())  # JSON hash no longer the recomputed one
+    # VerifySignatures never reads the JSON's lock_hash (lock.go:137-179): an
+    # edited JSON hash still verifies; VerifyHashes (lock_verify_hashes) rejects it
+    edited = dict(lock, lock_hash="0x" + bytes(32).hex())
+    dkg.lock_verify_signatures(edited, h, engine)
     with pytest.raises(dkg.DKGError, match="^invalid lock hash$"):
-        dkg.lock_verify_signatures(edited, h, engine)
-    wrong = bytes(32)  # a lock whose fields hash differently: same JSON hash and aggregate
-    with pytest.raises(dkg.DKGError, match="^invalid lock hash$"):
-        dkg.lock_verify_signatures(lock, wrong, engine)
-    unclaimed = {k: v for k, v in lock.items() if k != "lock_hash"}
+        dkg.lock_verify_hashes(edited, h)
+    dkg.lock_verify_hashes(lock, h)
+    wrong = bytes(32)  # a lock whose fields hash differently: same JSON and aggregate
     with pytest.raises(dkg.DKGError, match="^invalid lock signature aggregate$"):
-        dkg.lock_verify_signatures(unclaimed, wrong, engine)
+        dkg.lock_verify_signatures(lock, wrong, engine)
     missing = dict(lock, distributed_validators=lock["distributed_validators"][:-1])
     with pytest.raises(dkg.DKGError, match="^invalid lock signature aggregate$"):
         dkg.lock_verify_signatures(missing, h, engine)

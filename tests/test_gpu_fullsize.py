@@ -236,3 +236,56 @@ def test_submit_group_matches_single_batches(engine):
     # an empty group is refused (and nothing is left pending)
     with pytest.raises(eng.EngineError):
         engine.submit_group(eng.OP_VERIFY_AGGREGATE, [])
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(verify_mode=1),                                                     # level 3 only
+    dict(verify_mode=0, rlc_group=8, rlc_chunk=2, rlc_batch=2, rlc_seed=0x64),  # 1 -> 1.5 -> 1.5b -> 2b -> 3
+    dict(verify_mode=0, rlc_group=16, rlc_batch=2, rlc_seed=0x65, gident=1),  # level 1g, then level 3
+    dict(verify_mode=0, rlc_group=7, rlc_chunk=3, rlc_batch=1, rlc_seed=0x66, gident=2),  # level 0 fails; 1g -> 1.5
+], ids=["each", "g8c2", "g16_gid", "l0_g7c3_gid2"])
+def test_fallback_window_passes_match_oracle(cfg):
+    """The fallback levels share one line buffer of fb_window list positions,
+    consumed in passes (tbls_engine.hip, k_rlc.hip fb_passes).  With a
+    64-position window every level's list spans many passes (5 % invalid
+    partials: hundreds of chunks, duties and partials per level), and the
+    verdicts and aggregates must equal the one-pass default and oracle/c."""
+    from charon_amd import engine as eng
+    from tools.workload import make_batch
+    small = eng.Engine(0, slots=1, fb_window=64, **cfg)
+    wide = eng.Engine(0, slots=1, **cfg)
+    try:
+        b = make_batch(small, 3000, 3, 4, seed=64, inject=0.05)
+        wide.load_pubkeys(b.pubshares)  # same ids in both contexts (each loaded once)
+        t = small.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
+                         duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+        r_small = small.collect(t)
+        fb = small.fallback(t)
+        # at least one fallback list crossed the window
+        assert max(fb["chunks"], fb["chunk_searches"], fb["duty_searches"], fb["partial_checks"],
+                   fb["group_searches"]) > 64, fb
+        r_wide = engine_run(wide, b)
+        ref = oracle_run(b)
+        assert_same(r_small, ref)
+        assert_same(r_wide, ref)
+        assert np.array_equal(r_small.partial_status == eng.PS_VALID, ~b.injected)
+    finally:
+        small.close()
+        wide.close()
+
+
+def test_verify_each_past_the_default_window(engine):
+    """TBG_VERIFY_EACH with more partials than the default window (32,768):
+    level 3's list runs in two passes, invalid partials sit past position
+    32,768, and every verdict equals oracle/c."""
+    from charon_amd import engine as eng
+    from tools.workload import make_batch
+    each = eng.Engine(0, slots=1, verify_mode=eng.VERIFY_EACH)
+    try:
+        b = make_batch(each, 9000, 3, 4, seed=65, inject=0.01)
+        assert len(b.identifiers) > 32768 and b.injected[32768:].sum() >= 3
+        res = engine_run(each, b)
+        assert_same(res, oracle_run(b))
+        assert np.array_equal(res.partial_status == eng.PS_VALID, ~b.injected)
+    finally:
+        each.close()

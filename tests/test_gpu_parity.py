@@ -316,9 +316,8 @@ def test_level1g_resolves_single_bad_partials():
     level), with verdicts and aggregates exact; groups with several bad
     partials still reach the deeper levels and come out exact too."""
     from charon_amd import engine as eng
-    e = eng.Engine(0, verify_mode=0, rlc_group=8, rlc_chunk=4, rlc_batch=2, rlc_seed=0x1A)
-    prev = os.environ.get("TBG_GIDENT")
-    os.environ["TBG_GIDENT"] = "1"  # level 1g is opt-in (read by every submit)
+    # level 1g is opt-in (tbg_config.gident, fixed at init)
+    e = eng.Engine(0, verify_mode=0, rlc_group=8, rlc_chunk=4, rlc_batch=2, rlc_seed=0x1A, gident=eng.GIDENT_L3)
     try:
         b = _make_cluster_batch(e, 2000, 3, 4, seed=23, inject=0.01)
         t = e.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
@@ -337,19 +336,13 @@ def test_level1g_resolves_single_bad_partials():
         dev, pinned = e.slot_bytes(t)
         assert dev > 0 and pinned > 0
     finally:
-        if prev is None:
-            os.environ.pop("TBG_GIDENT", None)
-        else:
-            os.environ["TBG_GIDENT"] = prev
         e.close()
 
 
 def test_level1g_off_by_default_narrows_by_chunks(engine):
-    """Without TBG_GIDENT the failed groups take the chunk / duty narrowing
-    (level 1g is opt-in) and the verdicts are exact."""
+    """With the default tbg_config.gident (off) the failed groups take the
+    chunk / duty narrowing (level 1g is opt-in) and the verdicts are exact."""
     from charon_amd import engine as eng
-    if os.environ.get("TBG_GIDENT"):
-        pytest.skip("TBG_GIDENT set in the environment")
     b = _make_cluster_batch(engine, 600, 3, 4, seed=29, inject=0.02)
     t = engine.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
                       duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)

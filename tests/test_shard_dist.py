@@ -106,3 +106,35 @@ def test_shard_bounds_rules():
     assert shard_bounds(np.arange(11) * 4, 3) == [0, 4, 7, 10]       # 40 partials: cuts at 13, 26
     lo = shard_bounds(np.cumsum([0] + [4, 7, 10] * 50), 8)
     assert lo[0] == 0 and lo[-1] == 150 and all(a <= b for a, b in zip(lo, lo[1:]))
+
+
+def test_group_shard_bounds_cut_the_concatenation():
+    """tbg_multi_submit_group's cut (host mirror): several caller batches taken
+    back to back are cut like ONE batch, each ticket's layout is that cut
+    clamped to its own duties, and empty / zero-partial batches stay valid."""
+    from charon_amd.shard import group_shard_bounds, shard_bounds
+    rng = np.random.default_rng(5)
+    for trial in range(200):
+        k = int(rng.integers(1, 6))
+        dfs = []
+        for _ in range(k):
+            nd = int(rng.integers(1, 40))
+            counts = rng.integers(0, 11, size=nd) * (rng.random(nd) < 0.9)
+            dfs.append(np.concatenate([[0], np.cumsum(counts)]))
+        n = int(rng.integers(1, 10))
+        lays = group_shard_bounds(dfs, n)
+        glob = np.concatenate([d[:-1] + off for d, off in zip(dfs, np.cumsum([0] + [int(d[-1]) for d in dfs])[:-1])]
+                              + [[sum(int(d[-1]) for d in dfs)]])
+        cut = shard_bounds(glob, n)
+        base = 0
+        for d, lo in zip(dfs, lays):
+            nd = len(d) - 1
+            assert len(lo) == n + 1 and lo[0] == 0 and lo[-1] == nd
+            assert all(a <= b for a, b in zip(lo, lo[1:]))
+            assert lo == [min(max(c - base, 0), nd) for c in cut]
+            base += nd
+    # the config-4 shape: four batches of 1M 3-of-4 DVs -> eight 125k-DV shards
+    dfs = [np.arange(n + 1) * 4 for n in (400_000, 250_000, 250_000, 100_000)]
+    lays = group_shard_bounds(dfs, 8)
+    assert lays[0] == [0, 125_000, 250_000, 375_000] + [400_000] * 5
+    assert lays[3] == [0] * 8 + [100_000]

@@ -181,8 +181,7 @@ def main():
             "k_msm_bucket_part": {"per": "partial", "mads": round(4 * k_msm_entry)},
             "k_msm_bucket": {"per": "launch", "mads": round(bucket_scales + 32768 * (4 - 1) * g2_add)},
             "k_rlc_duty_sum<DSUM_L0_P>": {"per": "duty", "mads": round(duty_sum_p4)},
-            "k_rlc_miller_chunks<MILLER_L0>": {"per": "group", "mads": round(nch * chunk2), "plus_per_launch": s_quad},
-            # the same products on hexads (bls_hex.h, the default level-0 Miller kernel)
+            # the level-0 P-chunk products on hexads (bls_hex.h) + the one S hexad
             "k_miller_hex<MILLER_L0>": {"per": "group", "mads": round(nch * chunk2), "plus_per_launch": s_quad},
             "k_l0_fold": {"per": "group", "mads": round((nch - 1) * qmul)},
             "k_l0_final": {"per": "launch", "mads": round(final1)},

@@ -40,6 +40,7 @@ class ClusterBatch:
     shares: list             # per partial share scalars (ints)
     msgs: list               # per DV message bytes
     pk_first: int = 0        # resident id of pubshares[0] in the engine that loaded them
+    inject_kind: np.ndarray = None  # int8 [n_dv * n]: index into INJECT_KINDS, -1 if not injected (mixed batches)
 
 
 def _scalars(rng, count):
@@ -170,7 +171,7 @@ def make_mixed_batch(engine, n_dv, seed, inject=0.01, kinds=INJECT_KINDS, pool=N
         n_dv=n_dv, t=0, n=0, duty_first=duty_first, sigs=sigs, identifiers=ids, pubkey_ids=pubkey_ids,
         pubshares=pubshares, msg_data=np.frombuffer(b"".join(msgs), dtype=np.uint8), msg_off=msg_off,
         duty_msg=duty_msg, threshold=thr, group_sig=group_sig, injected=injected, expect_ok=valid_per_dv >= thr,
-        secrets=secrets, shares=shares, msgs=msgs, pk_first=int(first))
+        secrets=secrets, shares=shares, msgs=msgs, pk_first=int(first), inject_kind=kind_of.astype(np.int8))
 
 
 def make_batch(engine, n_dv, t, n, seed, inject=0.0, load=None):
