@@ -116,7 +116,7 @@ def work_model():
 STAGE_KERNELS = {
     "decode": ["k_decode_sigs", "k_subgroup_sigs"],
     "hash": ["k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
-    "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_bucket_part", "k_msm_sum", "k_msm_scan", "k_msm_scatter",
+    "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_bucket_part", "k_msm_tree", "k_msm_tree_final", "k_msm_scan", "k_msm_scatter",
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
                 "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>"],
     "h_lines": ["k_lines_h"],

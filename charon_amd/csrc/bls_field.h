@@ -77,6 +77,20 @@ namespace tbg {
 
 struct Fp { uint32_t l[NL]; };
 
+// Limbs: normalised values (every product, reduction and normalised sum)
+// have limbs < 2^28.  The LAZY sum / difference (fp_add_l, fp_sub_l) skip the
+// carry normalisation (39 of a normalised sum's 53 instructions) and leave
+// limbs < 2^31; such a value may feed fp_mul / fp_mul2 / fp_sqr (whose 64-bit
+// columns take the larger limbs, checked below), fp_reduce, fp_add_l, the
+// first operand of fp_sub(_l), fp_mul_small and limb-wise moves -- never the
+// second operand of a subtraction, fp_neg or a store that another kernel
+// reads as normalised.
+TBG_HD uint32_t fp_max_limb(const Fp& a) {
+  uint32_t m = 0;
+  for (int i = 0; i < NL; ++i) m = a.l[i] > m ? a.l[i] : m;
+  return m;
+}
+
 TBG_HD Fp fp_from_const(const uint32_t (&c)[NL]) {
   Fp r;
 #pragma unroll
@@ -122,6 +136,8 @@ TBG_HD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
 // >= 2^28 - 1, so no limb difference goes negative before normalisation.
 TBG_HD Fp fp_sub(const Fp& a, const Fp& b) {
   TBG_BOUND(fp_ratio_p(b) <= 16.0, "fp_sub b <= 16p");
+  TBG_BOUND(fp_max_limb(b) < (1u << 28), "fp_sub b normalised");
+  TBG_BOUND(fp_max_limb(a) < (1u << 31), "fp_sub a limbs < 2^31");
   Fp r;
 #pragma unroll
   for (int i = 0; i < NL; ++i) r.l[i] = a.l[i] + SUB16P_L[i] - b.l[i];
@@ -131,6 +147,7 @@ TBG_HD Fp fp_sub(const Fp& a, const Fp& b) {
 
 TBG_HD Fp fp_neg(const Fp& a) {
   TBG_BOUND(fp_ratio_p(a) <= 16.0, "fp_neg a <= 16p");
+  TBG_BOUND(fp_max_limb(a) < (1u << 28), "fp_neg a normalised");
   Fp r;
 #pragma unroll
   for (int i = 0; i < NL; ++i) r.l[i] = SUB16P_L[i] - a.l[i];
@@ -138,13 +155,40 @@ TBG_HD Fp fp_neg(const Fp& a) {
   return r;
 }
 
+// Lazy a + b and a + 16p - b (b normalised): the limbs are left unnormalised
+// (< 2^31, see the note at the top); value bounds as fp_add / fp_sub.
+TBG_HD Fp fp_add_l(const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = a.l[i] + b.l[i];
+  TBG_BOUND(fp_max_limb(r) < (1u << 31), "fp_add_l limbs < 2^31");
+  return r;
+}
+TBG_HD Fp fp_sub_l(const Fp& a, const Fp& b) {
+  TBG_BOUND(fp_ratio_p(b) <= 16.0, "fp_sub_l b <= 16p");
+  TBG_BOUND(fp_max_limb(b) < (1u << 28), "fp_sub_l b normalised");
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = a.l[i] + SUB16P_L[i] - b.l[i];
+  TBG_BOUND(fp_max_limb(r) < (1u << 31), "fp_sub_l limbs < 2^31");
+  return r;
+}
+// normalise the limbs of a lazy value (same value)
+TBG_HD Fp fp_norm(const Fp& a) {
+  Fp r = a;
+  fp_normalize(r);
+  return r;
+}
+
 // a - q p for q = floor(a/p) or floor(a/p) - 1: result in [0, 2p).
-// Valid for a < 2^390.
+// Valid for a < 2^390 with limbs < 2^31 (lazy sums included: the quotient
+// estimate ADDS the top limbs, so unpropagated carries still count).
 TBG_HD Fp fp_reduce(const Fp& a) {
   TBG_BOUND(a.l[NL - 1] < (1u << 26), "fp_reduce a < 2^390");
+  TBG_BOUND(fp_max_limb(a) < (1u << 31), "fp_reduce limbs < 2^31");
   TBG_COUNT(14);
   // top 60 bits: a >> 330  (limb 13 holds bits 364.., limb 12 bits 336.., limb 11 bits 308..)
-  uint64_t t = ((uint64_t)a.l[13] << 34) | ((uint64_t)a.l[12] << 6) | (uint64_t)(a.l[11] >> 22);
+  uint64_t t = ((uint64_t)a.l[13] << 34) + ((uint64_t)a.l[12] << 6) + (uint64_t)(a.l[11] >> 22);
   double q = (double)t * INV_PT - 1e-9;
   int32_t qi = q < 0.0 ? 0 : (int32_t)q;
   Fp r;
@@ -213,9 +257,22 @@ TBG_HD uint64_t acc_total(const uint64_t (&s)[N]) {
   else return s[0];
 }
 
+// Host checks: the largest column, sum_k a_i b_j over 14 K products, plus
+// the 14 m p products and the carry, must fit the 64-bit accumulator.
+TBG_HD bool fp_columns_fit(double ab_products) {
+  return ab_products + 14.0 * 268435456.0 * 268435456.0 + 68719476736.0 < 18446744073709551616.0;
+}
+
 template <int K>
 TBG_HD Fp fp_mul_sum(const Fp* const (&a)[K], const Fp* const (&b)[K]) {
   TBG_COUNT(196 * (K + 1));
+#if defined(TBG_BOUNDS_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+  {
+    double col = 0;
+    for (int n = 0; n < K; ++n) col += 14.0 * (double)fp_max_limb(*a[n]) * (double)fp_max_limb(*b[n]);
+    TBG_BOUND(fp_columns_fit(col), "fp_mul_sum columns fit 64 bits");
+  }
+#endif
   TBG_FENCE();
   uint32_t m[NL];
   Fp r;
@@ -271,6 +328,8 @@ TBG_HD Fp fp_mul2(const Fp& a, const Fp& b, const Fp& c, const Fp& d) {
 // split as in fp_mul_sum.
 TBG_HD Fp fp_sqr(const Fp& a) {
   TBG_BOUND(fp_ratio_p(a) * fp_ratio_p(a) < 2048.0, "fp_sqr bound");
+  TBG_BOUND(fp_max_limb(a) < (1u << 31), "fp_sqr limbs < 2^31");
+  TBG_BOUND(fp_columns_fit(8.0 * 2.0 * (double)fp_max_limb(a) * (double)fp_max_limb(a)), "fp_sqr columns fit");
   TBG_COUNT(301);
   TBG_FENCE();
   uint32_t a2[NL];

@@ -16,6 +16,7 @@ namespace tbg {
 
 template <int KIND>
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
+  if (KIND == FOLD_L0) TBG_URGENT();  // the one S of a level-0 launch: on its critical path
   // both lanes of a pair take the same branches; the fallback kinds run in
   // passes of fb_window list positions from fb_base (launch_rlc_check)
   const uint32_t k = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + (KIND == FOLD_GROUPS || KIND == FOLD_L0 ? 0u : B.fb_base);
@@ -35,7 +36,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
   } else if (KIND == FOLD_IDENT) {
     if (k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k) || (B.id_list[k] & ID_DEGENERATE)) return;
     out = B.id_lines;
-  } else {  // FOLD_L0: level 0's S (k_msm_sum)
+  } else {  // FOLD_L0: level 0's S (k_msm_tree_final)
     if (k != 0 || B.counters[CNT_L0_BAD]) return;
     const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
     px_g2_lines(px_load(*B.batch_pt), nx, fp_from_const(G1_NEG_Y), B.batch_lines);

@@ -17,7 +17,7 @@
 //   k_msm_scatter    bucket entries
 //   k_msm_bucket_part  one lane PAIR per quarter of a bucket: its sum
 //   k_msm_bucket     one lane PAIR per bucket: the quarters' sum times (2j + 1)
-//   k_msm_sum        tree sums (fan-in 16), the last one in affine form
+//   k_msm_tree, k_msm_tree_final  the sum of the scaled buckets (LDS trees), S affine
 #define TBG_ADD_DBL_INLINE 1
 #ifndef TBG_SCHED_FENCE
 #define TBG_SCHED_FENCE 1  // products in program order: fits the pair kernels in 256 VGPRs (bls_field.h)
@@ -78,6 +78,7 @@ __global__ void TBG_LAUNCH k_rlc_g1_l0(DevBatch B, const G1A* tab, const int32_t
 // (msm_cur): one workgroup of 1024 lanes, 32 buckets per lane.
 constexpr int kScanBlock = 1024;
 __global__ void __launch_bounds__(kScanBlock) k_msm_scan(DevBatch B) {
+  TBG_URGENT();
   __shared__ uint32_t part[kScanBlock];
   constexpr uint32_t per = MSM_BUCKETS / kScanBlock;
   const uint32_t t = threadIdx.x, j0 = t * per;
@@ -147,6 +148,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket_part(DevBatch B) {
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
+  TBG_URGENT();
   const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (j >= MSM_BUCKETS) return;
   if (B.counters[CNT_L0_BAD]) return;
@@ -166,22 +168,55 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
   px_store(B.msm_bkt[j], acc);
 }
 
-// Tree sum: lane pair t adds points [16 t, 16 t + 16) of `in` (n of them).
-// The last pass (n <= 16) writes S in affine form, or flags level 0 when S
-// is the point at infinity.
-__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_sum(DevBatch B, const G2J* in, uint32_t n, G2J* out) {
-  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
-  const uint32_t a0 = t * MSM_SUM_FAN;
-  if (a0 >= n) return;
-  if (B.counters[CNT_L0_BAD]) return;
-  const uint32_t a1 = min(a0 + MSM_SUM_FAN, n);
-  Jac<Fp2x> acc = px_load(in[a0]);
+// Tree sum of the scaled buckets in TWO kernels (four passes of 16-point
+// chains took 60 dependent additions, ~1.8 ms of a launch's critical path):
+// a lane pair adds MSM_TREE_PER points, then the workgroup halves its pairs
+// through LDS (log2 levels); the first kernel leaves one point per
+// workgroup, the second sums those the same way and writes S in affine form
+// (or flags level 0 when S is the point at infinity): 3 + 7 + 1 + 5 = 16
+// dependent additions.
+constexpr uint32_t MSM_TREE_PAIRS = 128;  // lane pairs per workgroup of the first kernel
+constexpr uint32_t MSM_TREE_PER = 4;      // points per pair in the first kernel
+constexpr uint32_t MSM_TREE_WG = MSM_BUCKETS / (MSM_TREE_PAIRS * MSM_TREE_PER);  // 64 partial sums
+static_assert(MSM_TREE_WG <= 2 * 64 && MSM_TREE_WG <= MSM_SUM_ENTRIES, "second tree kernel: one workgroup");
+
+// acc summed over the workgroup's PAIRS lane pairs (every thread calls it;
+// pair 0 ends with the total)
+template <uint32_t PAIRS>
+__device__ __forceinline__ Jac<Fp2x> pair_tree_sum(Jac<Fp2x> acc, Jac<Fp2x>* lds) {
+  const uint32_t t = threadIdx.x, pr = t >> 1;
 #pragma unroll 1
-  for (uint32_t a = a0 + 1; a < a1; ++a) acc = jac_add_in<Fp2x, true>(acc, px_load(in[a]));
-  if (n > MSM_SUM_FAN) {
-    px_store(out[t], acc);
-    return;
+  for (uint32_t s = 1; s < PAIRS; s <<= 1) {
+    lds[t] = acc;
+    __syncthreads();
+    if ((pr & (2 * s - 1)) == 0 && pr + s < PAIRS) acc = jac_add_in<Fp2x, true>(acc, lds[t + 2 * s]);
+    __syncthreads();
   }
+  return acc;
+}
+
+__global__ void __launch_bounds__(2 * MSM_TREE_PAIRS) k_msm_tree(DevBatch B) {
+  TBG_URGENT();
+  __shared__ Jac<Fp2x> lds[2 * MSM_TREE_PAIRS];
+  if (B.counters[CNT_L0_BAD]) return;  // (grid-uniform)
+  const uint32_t pr = threadIdx.x >> 1;
+  const uint32_t a0 = (blockIdx.x * MSM_TREE_PAIRS + pr) * MSM_TREE_PER;
+  Jac<Fp2x> acc = px_load(B.msm_bkt[a0]);
+#pragma unroll 1
+  for (uint32_t a = a0 + 1; a < a0 + MSM_TREE_PER; ++a) acc = jac_add_in<Fp2x, true>(acc, px_load(B.msm_bkt[a]));
+  acc = pair_tree_sum<MSM_TREE_PAIRS>(acc, lds);
+  if (pr == 0) px_store(B.msm_sum[blockIdx.x], acc);
+}
+
+__global__ void __launch_bounds__(MSM_TREE_WG) k_msm_tree_final(DevBatch B) {
+  TBG_URGENT();
+  constexpr uint32_t PAIRS = MSM_TREE_WG / 2;
+  __shared__ Jac<Fp2x> lds[2 * PAIRS];
+  if (B.counters[CNT_L0_BAD]) return;
+  const uint32_t pr = threadIdx.x >> 1;
+  Jac<Fp2x> acc = jac_add_in<Fp2x, true>(px_load(B.msm_sum[2 * pr]), px_load(B.msm_sum[2 * pr + 1]));
+  acc = pair_tree_sum<PAIRS>(acc, lds);
+  if (pr != 0) return;
   if (jac_is_inf(acc)) {
     if (pair_par() == 0) B.counters[CNT_L0_BAD] = 1;  // S = 0: no lines; the group levels decide
     return;
@@ -196,25 +231,21 @@ void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, 
                      tab);
 }
 
-// Level 0 up to S's lines: G1 products and P_d (k_rlc_duty_sum), then the MSM.
-void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
+// Level 0's key side: G1 products, bucket sizes, and the ERR_PUBKEY marks
+// (after it the candidates are final: the speculative aggregation may run).
+void launch_l0_keys(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
   // (msm_off was zeroed by k_decode_sigs, the chain's first kernel)
   if (B.n_partials) TBG_KLAUNCH(k_rlc_g1_l0, grid_for(B.n_partials), dim3(kBlock), st, B, pk_tab, pk_status, n_pk);
+}
+
+// Level 0's signature side: the bucket MSM up to S (affine).
+void launch_l0_msm(const DevBatch& B, hipStream_t st) {
   TBG_KLAUNCH(k_msm_scan, dim3(1), dim3(kScanBlock), st, B);
   if (B.n_partials) TBG_KLAUNCH(k_msm_scatter, grid_for(B.n_partials), dim3(kBlock), st, B);
   TBG_KLAUNCH(k_msm_bucket_part, grid_for(2 * MSM_BUCKETS * MSM_SPLIT), dim3(kBlock), st, B);
   TBG_KLAUNCH(k_msm_bucket, grid_for(2 * MSM_BUCKETS), dim3(kBlock), st, B);
-  const G2J* in = B.msm_bkt;
-  uint32_t n = MSM_BUCKETS;
-  G2J* out = B.msm_sum;
-  while (true) {
-    const uint32_t m = (n + MSM_SUM_FAN - 1) / MSM_SUM_FAN;
-    TBG_KLAUNCH(k_msm_sum, grid_for(2 * m), dim3(kBlock), st, B, in, n, out);
-    if (n <= MSM_SUM_FAN) break;
-    in = out;
-    out += m;
-    n = m;
-  }
+  TBG_KLAUNCH(k_msm_tree, dim3(MSM_TREE_WG), dim3(2 * MSM_TREE_PAIRS), st, B);
+  TBG_KLAUNCH(k_msm_tree_final, dim3(1), dim3(MSM_TREE_WG), st, B);
 }
 
 }  // namespace tbg

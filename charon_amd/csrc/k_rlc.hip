@@ -239,6 +239,7 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
 // One quad per group: the product of its P-chunk values (k_rlc_miller_chunks,
 // MILLER_L0); a combined duty whose H(m) is unusable makes level 0 fail.
 __global__ void TBG_LAUNCH_N(2) k_l0_fold(DevBatch B) {
+  TBG_URGENT();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk;
   const uint32_t n_groups = (B.n_duties + G - 1) / G, nch = (G + C - 1) / C, nq = nch + 1;
@@ -259,6 +260,7 @@ __global__ void TBG_LAUNCH_N(2) k_l0_fold(DevBatch B) {
 
 // Product tree, one quad per L0_TREE_FAN values of grp_f[in .. in + n).
 __global__ void TBG_LAUNCH_N(2) k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32_t out) {
+  TBG_URGENT();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t q = fp12_slot(t), a0 = q * L0_TREE_FAN;
   if (a0 >= n || B.counters[CNT_L0_BAD]) return;
@@ -280,6 +282,7 @@ struct WideDevExec {
   }
 };
 __global__ void __launch_bounds__(64) k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
+  TBG_URGENT();
   if (B.counters[CNT_L0_BAD]) return;  // (workgroup-uniform)
   __shared__ WideSlots S;
   WideDevExec ex;
@@ -865,19 +868,24 @@ static void fb_passes(const DevBatch& B, uint32_t max_entries, F&& body) {
 }
 
 void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const G1A* pk_tab,
-                        const int32_t* pk_status, uint32_t n_pk, hipStream_t st) {
+                        const int32_t* pk_status, uint32_t n_pk, hipStream_t st,
+                        void (*after_keys)(const DevBatch&, hipStream_t)) {
   if (!B.n_duties) return;
   if (B.rlc_group == 0) {
     if (B.n_partials) TBG_KLAUNCH(k_list_all_partials, grid_for(B.n_partials), dim3(kBlock), st, B, pk_status, n_pk);
+    if (after_keys) after_keys(B, st);
     return;
   }
   uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
   if (B.rlc_batch) {  // level 0: G1 products, P_d, the signature MSM and S's lines
-    launch_l0_prepare(B, pk_tab, pk_status, n_pk, st);
+    launch_l0_keys(B, pk_tab, pk_status, n_pk, st);
+    if (after_keys) after_keys(B, st);
+    launch_l0_msm(B, st);
     TBG_KLAUNCH(k_rlc_duty_sum<DSUM_L0_P>, duty_grid(B), dim3(BINV_BLOCK), st, B);
     launch_lines_fold(B, FOLD_L0, 1, st);
     return;
   }
+  if (after_keys) after_keys(B, st);
   launch_rlc_partials(B, pk_tab, pk_aff, pk_status, n_pk, st);
   TBG_KLAUNCH(k_rlc_duty_sum<DSUM_BOTH>, duty_grid(B), dim3(BINV_BLOCK), st, B);
   TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);

@@ -369,6 +369,15 @@ ready:
   return rc;
 }
 
+// Level 0 on: the aggregation a level-0 pass will confirm (every candidate
+// valid), enqueued mid-chain so the launch's tail is the verification alone;
+// the regular aggregation after the checks returns at once after a pass.
+static void spec_aggregation(const DevBatch& B, hipStream_t st) {
+  launch_lagrange(B, st, true);
+  launch_aggregate(B, st, true);
+  launch_aggregate_finish(B, st, true);
+}
+
 // The kernel chain of one batch.  Per-message work (hash_to_G2, H(m) lines)
 // runs on st2 concurrently with the per-signature work (decode, RLC sums and
 // group lines) on st; the product checks join both.
@@ -387,9 +396,6 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   // With one stream per slot the two independent chains run one after the
   // other, the per-message chain first (running the per-signature chain
   // first on odd slots was measured no better, round 2).
-  // Level 0 on: aggregate speculatively (every candidate valid) in the
-  // middle of the chain, so the launch's tail is the verification alone; the
-  // regular aggregation below returns at once after a level-0 pass.
   const bool spec = B.op == TBG_OP_VERIFY_AGGREGATE && B.rlc_batch && B.rlc_group;
   auto msg_chain = [&]() -> int {
     HIP_TRY(hipEventRecord(ev[3], st2));
@@ -403,14 +409,15 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
     HIP_TRY(hipEventRecord(ev[10], st));
     launch_decode_sigs(B, st);  // zeroes B.counters (and level 0's bucket sizes) first
     HIP_TRY(hipEventRecord(ev[1], st));
+    // The aggregation a level-0 pass will confirm runs as soon as the
+    // candidates are final (after the key checks), before the bucket MSM:
+    // placed after it, its small kernels waited behind the other launches'
+    // long Miller waves for a free slot and delayed this launch's own Miller
+    // kernel (k_lagrange<true> 7.7 ms instead of 0.05, profiles/r04/base/
+    // timeline_s20.txt).
     if (verify)
       launch_rlc_prepare(B, pk, (const G1A*)c->d_xpk, (const G1A*)c->d_pktab, (const int32_t*)c->d_pk_status, c->n_pk,
-                         st);
-    if (spec) {  // the aggregation a level-0 pass will confirm, before the verification tail
-      launch_lagrange(B, st, true);
-      launch_aggregate(B, st, true);
-      launch_aggregate_finish(B, st, true);
-    }
+                         st, spec ? spec_aggregation : nullptr);
     HIP_TRY(hipEventRecord(ev[2], st));
     return TBG_OK;
   };

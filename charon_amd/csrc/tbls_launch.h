@@ -34,6 +34,18 @@ constexpr int kBlock = 64;
 #define TBG_DECODE_WAVES 2  // k_decode_sigs (square roots only)
 #endif
 #define TBG_LAUNCH_N(w) __launch_bounds__(64, w)
+// Latency-critical kernels of a launch's serial tail (the level-0 bucket
+// reduction, S's lines, the product tree, the one final exponentiation) run
+// a few waves each, often on SIMDs that also host other launches' long
+// Miller / decode waves, which halve their issue rate (k_l0_final 3.4 ms
+// alone, 6.8 ms beside a Miller kernel, profiles/r04/base/timeline_s20.txt).
+// s_setprio 3 makes their waves win the SIMD's instruction arbitration;
+// the throughput kernels lose nothing but the slots these few waves use.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TBG_URGENT() __builtin_amdgcn_s_setprio(3)
+#else
+#define TBG_URGENT() ((void)0)
+#endif
 inline dim3 grid_for(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
 // Device-side layout of one batch (all pointers into device memory).
@@ -135,11 +147,11 @@ enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS =
                      CNT_L0_OK = 6, CNT_GID = 7, CNT_WORDS = 8 };  // CNT_GID: level-1g groups
 
 // Level-0 MSM: a digit a (odd, |a| < 2^16) of r_i puts psi^k(s_i) into bucket
-// (|a| - 1) / 2; the tree sums fold MSM_SUM_FAN points per thread.
+// (|a| - 1) / 2; the tree sums (k_msm_tree) leave one point per workgroup in
+// msm_sum.
 constexpr uint32_t MSM_BUCKETS = 32768;
-constexpr uint32_t MSM_SUM_FAN = 16;
 constexpr uint32_t MSM_SPLIT = 4;  // slices per bucket (k_msm_bucket_part)
-constexpr uint32_t MSM_SUM_ENTRIES = MSM_BUCKETS / MSM_SUM_FAN + MSM_BUCKETS / (MSM_SUM_FAN * MSM_SUM_FAN) + 16;
+constexpr uint32_t MSM_SUM_ENTRIES = 128;
 // Level-0 product tree over the groups' P-chunk products.  Each pass is a
 // chain of F - 1 Fp12 products on one lane group (~24 us each at one wave per
 // SIMD), so the tree's latency ~ log_F(n) * F is smallest near F = 4 (16: 1.3
@@ -211,14 +223,19 @@ void launch_decode_sigs(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);
 void launch_hash_clear(const DevBatch& B, hipStream_t st);
 void launch_h_lines(const DevBatch& B, hipStream_t st);
+// after_keys (optional) is enqueued once the candidates are final (the
+// ERR_PUBKEY marks made), before the level-0 bucket MSM: the chain's
+// speculative aggregation goes there, off the Miller kernel's critical path
 void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const G1A* pk_tab,
-                        const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+                        const int32_t* pk_status, uint32_t n_pk, hipStream_t st,
+                        void (*after_keys)(const DevBatch&, hipStream_t) = nullptr);
 void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, const int32_t* pk_status, uint32_t n_pk,
                       hipStream_t st);
 void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStream_t st);
 // level 0 (k_msm.hip)
 void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab, hipStream_t st);
-void launch_l0_prepare(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+void launch_l0_keys(const DevBatch& B, const G1A* pk_tab, const int32_t* pk_status, uint32_t n_pk, hipStream_t st);
+void launch_l0_msm(const DevBatch& B, hipStream_t st);
 void launch_l0_check(const DevBatch& B, hipStream_t st);
 // level 0's P-chunk and S Miller products on hexads (k_miller_hex.hip)
 void launch_l0_miller_hex(const DevBatch& B, hipStream_t st);
