@@ -16,6 +16,15 @@ TBG_HD Fp f_add(const Fp& a, const Fp& b) { return fp_add(a, b); }
 TBG_HD Fp2 f_add(const Fp2& a, const Fp2& b) { return fp2_add(a, b); }
 TBG_HD Fp f_sub(const Fp& a, const Fp& b) { return fp_sub(a, b); }
 TBG_HD Fp2 f_sub(const Fp2& a, const Fp2& b) { return fp2_sub(a, b); }
+// Lazy sum / difference (limbs left unnormalised, bls_field.h): for results
+// that only feed f_reduce, the FIRST operand of f_mul / f_mulfp / f_mulc, the
+// first operand of f_sub(_l) or f_small -- never f_sqr (its lane pieces
+// subtract the operand's halves), the second operand of f_mul (negated) or
+// of a subtraction, or a stored coordinate.
+TBG_HD Fp f_add_l(const Fp& a, const Fp& b) { return fp_add_l(a, b); }
+TBG_HD Fp2 f_add_l(const Fp2& a, const Fp2& b) { return {fp_add_l(a.c0, b.c0), fp_add_l(a.c1, b.c1)}; }
+TBG_HD Fp f_sub_l(const Fp& a, const Fp& b) { return fp_sub_l(a, b); }
+TBG_HD Fp2 f_sub_l(const Fp2& a, const Fp2& b) { return {fp_sub_l(a.c0, b.c0), fp_sub_l(a.c1, b.c1)}; }
 TBG_HD Fp f_neg(const Fp& a) { return fp_neg(a); }
 TBG_HD Fp2 f_neg(const Fp2& a) { return fp2_neg(a); }
 TBG_HD Fp f_mul(const Fp& a, const Fp& b) { return fp_mul(a, b); }
@@ -58,14 +67,14 @@ template <class F> TBG_HD Jac<F> jac_dbl_in(const Jac<F>& p) {
   F A = f_sqr(p.X);
   F B = f_sqr(p.Y);
   F C = f_sqr(B);
-  F t = f_sub(f_sqr(f_add(p.X, B)), f_add(A, C));   // < 18p
-  F D = f_reduce(f_add(t, t));
+  F t = f_sub_l(f_sqr(f_add(p.X, B)), f_add(A, C));   // < 18p
+  F D = f_reduce(f_add_l(t, t));
   F E = f_small(A, 3);                                // < 6p
   F Fv = f_sqr(E);
-  F X3 = f_reduce(f_sub(Fv, f_add(D, D)));
-  F Y3 = f_reduce(f_sub(f_mul(f_sub(D, X3), E), f_small(C, 8)));  // bigger operand first (fp2_mul negates b.c1)
+  F X3 = f_reduce(f_sub_l(Fv, f_add(D, D)));
+  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(D, X3), E), f_small(C, 8)));  // bigger operand first (fp2_mul negates b.c1)
   F YZ = f_mul(p.Y, p.Z);
-  F Z3 = f_reduce(f_add(YZ, YZ));
+  F Z3 = f_reduce(f_add_l(YZ, YZ));
   return {X3, Y3, Z3};
 }
 
@@ -90,8 +99,8 @@ template <class F, bool INLDBL = false> TBG_HD Jac<F> jac_add_in(const Jac<F>& p
   F U2 = f_mul(q.X, Z1Z1);
   F S1 = f_mul(f_mul(p.Y, q.Z), Z2Z2);
   F S2 = f_mul(f_mul(q.Y, p.Z), Z1Z1);
-  F H = f_reduce(f_sub(U2, U1));
-  F Rr = f_reduce(f_sub(S2, S1));
+  F H = f_reduce(f_sub_l(U2, U1));
+  F Rr = f_reduce(f_sub_l(S2, S1));
   if (f_is_zero(H)) {
     if (f_is_zero(Rr)) return INLDBL ? jac_dbl_in(p) : jac_dbl(p);
     return jac_inf<F>();
@@ -101,9 +110,9 @@ template <class F, bool INLDBL = false> TBG_HD Jac<F> jac_add_in(const Jac<F>& p
   F J = f_mul(H, I);
   F r2 = f_add(Rr, Rr);
   F V = f_mul(U1, I);
-  F X3 = f_reduce(f_sub(f_sub(f_sqr(r2), J), f_add(V, V)));
-  F Y3 = f_reduce(f_sub(f_mul(f_sub(V, X3), r2), f_small(f_mul(S1, J), 2)));
-  F Zs = f_sub(f_sqr(f_add(p.Z, q.Z)), f_add(Z1Z1, Z2Z2));   // < 18p
+  F X3 = f_reduce(f_sub_l(f_sub_l(f_sqr(r2), J), f_add(V, V)));
+  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(V, X3), r2), f_small(f_mul(S1, J), 2)));
+  F Zs = f_sub_l(f_sqr(f_add(p.Z, q.Z)), f_add(Z1Z1, Z2Z2));   // < 18p
   F Z3 = f_mul(f_reduce(Zs), H);
   return {X3, Y3, Z3};
 }
@@ -114,8 +123,8 @@ template <class F> TBG_HD Jac<F> jac_add_aff_in(const Jac<F>& p, const Aff<F>& q
   F Z1Z1 = f_sqr(p.Z);
   F U2 = f_mul(q.x, Z1Z1);
   F S2 = f_mul(f_mul(q.y, p.Z), Z1Z1);
-  F H = f_reduce(f_sub(U2, p.X));
-  F Rr = f_reduce(f_sub(S2, p.Y));
+  F H = f_reduce(f_sub_l(U2, p.X));
+  F Rr = f_reduce(f_sub_l(S2, p.Y));
   if (f_is_zero(H)) {
     if (f_is_zero(Rr)) return TBG_ADD_DBL(p);
     return jac_inf<F>();
@@ -125,9 +134,9 @@ template <class F> TBG_HD Jac<F> jac_add_aff_in(const Jac<F>& p, const Aff<F>& q
   F J = f_mul(H, I);
   F r2 = f_add(Rr, Rr);
   F V = f_mul(p.X, I);
-  F X3 = f_reduce(f_sub(f_sub(f_sqr(r2), J), f_add(V, V)));
-  F Y3 = f_reduce(f_sub(f_mul(f_sub(V, X3), r2), f_small(f_mul(p.Y, J), 2)));
-  F Z3 = f_reduce(f_sub(f_sub(f_sqr(f_add(p.Z, H)), Z1Z1), HH));
+  F X3 = f_reduce(f_sub_l(f_sub_l(f_sqr(r2), J), f_add(V, V)));
+  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(V, X3), r2), f_small(f_mul(p.Y, J), 2)));
+  F Z3 = f_reduce(f_sub_l(f_sub_l(f_sqr(f_add(p.Z, H)), Z1Z1), HH));
   return {X3, Y3, Z3};
 }
 

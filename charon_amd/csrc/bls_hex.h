@@ -12,9 +12,9 @@
 // half the live state, so the kernel fits 256 VGPRs: two waves per SIMD.
 //
 // Layout: trio lane q = (lane & 15) % 3 as in bls_quad.h (5 trios per DPP
-// row, lane 15 idle) in BOTH halves of the wave; component c = lane >> 5
-// (lanes 0..31 hold c0, lanes 32..63 c1, partner = lane ^ 32, one
-// v_permlane32_swap per word).  Trio exchanges stay DPP row shifts on the
+// row, lane 15 idle); component c = (lane >> 4) & 1 (rows 0 and 2 hold c0,
+// rows 1 and 3 c1, partner = lane ^ 16, one ds_swizzle per word; see
+// TBG_HEX_SWIZZLE below for the permlane32 form).  Trio exchanges stay DPP row shifts on the
 // own component.  A wave carries 10 Fp12 values (60 of 64 lanes work).
 //
 // Cross-component terms (the multiplications by xi = 1 + u hidden in the
@@ -41,15 +41,22 @@ struct Fp4o { Fp2o a, b; };
 
 TBG_HD Fp4h hx_select(bool k, const Fp4h& x, const Fp4h& y) { return {fp_select(k, x.a, y.a), fp_select(k, x.b, y.b)}; }
 TBG_HD Fp2o hx_add(const Fp2o& x, const Fp2o& y) { return {fp_add(x.o, y.o), fp_add(x.p, y.p)}; }
+// lazy (bls_field.h): for the FIRST operand of hx_mul only
+TBG_HD Fp2o hx_add_l(const Fp2o& x, const Fp2o& y) { return {fp_add_l(x.o, y.o), fp_add_l(x.p, y.p)}; }
 // xi x = (x0 - x1) + (x0 + x1) u seen from lane c (lazy: < x + 16p)
+// (lazy limbs: only ever the first operand of a lazy sum that feeds hx_mul's
+// first operand)
 TBG_HD Fp2o hx_mul_xi(uint32_t c, const Fp2o& x) {
-  const Fp s = fp_add(x.o, x.p), d0 = fp_sub(x.o, x.p), d1 = fp_sub(x.p, x.o);
+  const Fp s = fp_add_l(x.o, x.p), d0 = fp_sub_l(x.o, x.p), d1 = fp_sub_l(x.p, x.o);
   return {fp_select(c != 0, s, d0), fp_select(c != 0, d1, s)};
 }
 // component c of x y (one REDC(ab + cd)); x < 32p, y's partner < 16p
 TBG_HD Fp hx_mul(uint32_t c, const Fp2o& x, const Fp2o& y) { return pair_mul_lane(c, x.o, x.p, y.o, y.p); }
 // component c of xi x from x's own / partner components (lazy: < x0 + 16p)
-TBG_HD Fp hx_xi(uint32_t c, const Fp& own, const Fp& par) { return pair_mul_xi_lane(c, own, par); }
+// (lazy limbs: every use feeds a lazy sum into fp_reduce)
+TBG_HD Fp hx_xi(uint32_t c, const Fp& own, const Fp& par) {
+  return fp_select(c != 0, fp_add_l(own, par), fp_sub_l(own, par));
+}
 // host tests: lane c's view of a whole value
 TBG_HD Fp2o hx_view(uint32_t c, const Fp2& x) { return c ? Fp2o{x.c1, x.c0} : Fp2o{x.c0, x.c1}; }
 TBG_HD Fp4o hx_view4(uint32_t c, const Fp4& x) { return {hx_view(c, x.a), hx_view(c, x.b)}; }
@@ -60,12 +67,12 @@ TBG_HD Fp4o hx_view4(uint32_t c, const Fp4& x) { return {hx_view(c, x.a), hx_vie
 // the right one's partner component, which must stay < 16p)
 TBG_HD void hx_sqr1(uint32_t c, const Fp4o& x, Fp& ab, Fp& s) {
   ab = hx_mul(c, x.a, x.b);
-  s = hx_mul(c, hx_add(x.a, hx_mul_xi(c, x.b)), hx_add(x.a, x.b));
+  s = hx_mul(c, hx_add_l(x.a, hx_mul_xi(c, x.b)), hx_add(x.a, x.b));
 }
 // phase 2 (ab's partner component abp): component c of {t0, reduce(t1)}
 TBG_HD Fp4h hx_sqr2(uint32_t c, const Fp& ab, const Fp& abp, const Fp& s) {
-  const Fp u = fp_reduce(fp_add(ab, hx_xi(c, ab, abp)));
-  return {fp_reduce(fp_sub(s, u)), fp_reduce(fp_add(ab, ab))};
+  const Fp u = fp_reduce(fp_add_l(hx_xi(c, ab, abp), ab));
+  return {fp_reduce(fp_sub_l(s, u)), fp_reduce(fp_add_l(ab, ab))};
 }
 
 // ---- quad_combine for component c.  Phase 1: T and V, the value whose xi
@@ -74,7 +81,7 @@ TBG_HD Fp4h hx_sqr2(uint32_t c, const Fp& ab, const Fp& abp, const Fp& s) {
 TBG_HD void hx_comb1(int q, const Fp4h& P, const Fp4h& Pn, const Fp4h& Pp, const Fp4h& Qx, Fp4h& T, Fp& V) {
   const Fp4h f1 = hx_select(q == 1, Pp, Pn);
   const Fp4h f2 = hx_select(q == 0, Pp, P);
-  T = {fp_reduce(fp_sub(Qx.a, fp_add(f1.a, f2.a))), fp_reduce(fp_sub(Qx.b, fp_add(f1.b, f2.b)))};
+  T = {fp_reduce(fp_sub_l(Qx.a, fp_add(f1.a, f2.a))), fp_reduce(fp_sub_l(Qx.b, fp_add(f1.b, f2.b)))};
   V = fp_select(q == 0, T.b, Pn.b);
 }
 TBG_HD Fp4h hx_comb2(uint32_t c, int q, const Fp4h& P, const Fp4h& Pn, const Fp4h& Pp, const Fp4h& T, const Fp& V,
@@ -85,7 +92,7 @@ TBG_HD Fp4h hx_comb2(uint32_t c, int q, const Fp4h& P, const Fp4h& Pn, const Fp4
   const Fp y0 = fp_select(q == 0, P.a, fp_select(q == 1, xv, Pp.a));
   const Fp x1 = fp_select(q == 0, T.a, T.b);
   const Fp y1 = fp_select(q == 0, P.b, fp_select(q == 1, Pn.a, Pp.b));
-  return {fp_reduce(fp_add(x0, y0)), fp_reduce(fp_add(x1, y1))};
+  return {fp_reduce(fp_add_l(x0, y0)), fp_reduce(fp_add_l(x1, y1))};
 }
 
 // ---- f * line, line = L0 + L2 x^2 with L0 = (l0, l4), L2 = l1 (evaluated):
@@ -100,15 +107,67 @@ TBG_HD void hx_line_u(uint32_t c, const Fp4o& An, const Fp2o& l1, HxLine& r) {
 TBG_HD void hx_line_t(uint32_t c, int q, const Fp4o& A, const Fp2o& l0, const Fp2o& l4, HxLine& r) {
   r.t0 = hx_mul(c, A.a, l0);
   r.t1 = hx_mul(c, A.b, l4);
-  r.s = hx_mul(c, hx_add(A.a, A.b), hx_add(l0, l4));
+  r.s = hx_mul(c, hx_add_l(A.a, A.b), hx_add(l0, l4));
   r.W = fp_add(r.t1, fp_select(q < 2, r.ub, fp_zero()));
 }
 // phase 2 (W's partner component Wp)
 TBG_HD Fp4h hx_line2(uint32_t c, int q, const HxLine& r, const Fp& Wp) {
   const Fp xw = hx_xi(c, r.W, Wp);                                 // < 20p
-  const Fp ca = fp_reduce(fp_add(fp_add(r.t0, xw), fp_select(q < 2, fp_zero(), r.ua)));
-  const Fp c1 = fp_sub(r.s, fp_add(r.t0, r.t1));                   // < 18p
-  return {ca, fp_reduce(fp_add(c1, fp_select(q < 2, r.ua, r.ub)))};
+  const Fp ca = fp_reduce(fp_add_l(fp_add_l(xw, r.t0), fp_select(q < 2, fp_zero(), r.ua)));
+  const Fp c1 = fp_sub_l(r.s, fp_add(r.t0, r.t1));                 // < 18p
+  return {ca, fp_reduce(fp_add_l(c1, fp_select(q < 2, r.ua, r.ub)))};
+}
+
+// ---- fp4_mul(x, y) = (x.a y.a + xi x.b y.b, (x.a + x.b)(y.a + y.b) - x.a y.a
+// - x.b y.b), the trio's Karatsuba over Fp4, in two phases around one exchange.
+// phase 1: component c of t0 = x.a y.a, t1 = x.b y.b, s = (x.a + x.b)(y.a + y.b)
+TBG_HD void hx_mul1(uint32_t c, const Fp4o& x, const Fp4o& y, Fp& t0, Fp& t1, Fp& s) {
+  t0 = hx_mul(c, x.a, y.a);
+  t1 = hx_mul(c, x.b, y.b);
+  s = hx_mul(c, hx_add_l(x.a, x.b), hx_add(y.a, y.b));
+}
+// phase 2 (t1's partner component t1p)
+TBG_HD Fp4h hx_mul2(uint32_t c, const Fp& t0, const Fp& t1, const Fp& t1p, const Fp& s) {
+  return {fp_reduce(fp_add_l(hx_xi(c, t1, t1p), t0)), fp_reduce(fp_sub_l(s, fp_add(t0, t1)))};
+}
+
+// ---- cyclotomic squaring (quad_cyc_lane) for component c: Tx = fp4_sqr of
+// trio lane {0, 2, 1}[q]'s coefficient, Txbp = the partner component of Tx.b
+TBG_HD Fp4h hx_cyc(uint32_t c, int q, const Fp4h& A, const Fp4h& Tx, const Fp& Txbp) {
+  const Fp s1 = fp_select(q == 1, fp_reduce(hx_xi(c, Tx.b, Txbp)), Tx.a);
+  const Fp s2 = fp_select(q == 1, Tx.a, Tx.b);
+  const Fp a2 = fp_add(A.a, A.a), b2 = fp_add(A.b, A.b);
+  const Fp s13 = fp_mul_small(s1, 3), s23 = fp_mul_small(s2, 3);
+  const Fp na = fp_select(q == 1, fp_add_l(s13, a2), fp_sub_l(s13, a2));
+  const Fp nb = fp_select(q == 1, fp_sub_l(s23, b2), fp_add_l(s23, b2));
+  return {fp_reduce(na), fp_reduce(nb)};
+}
+
+// ---- conj (w -> -w: negate a_1, a_3, a_5), component-wise
+TBG_HD Fp4h hx_conj(int q, const Fp4h& A) {
+  const Fp na = fp_reduce(fp_neg(A.a)), nb = fp_reduce(fp_neg(A.b));
+  return {fp_select(q == 1, na, A.a), fp_select(q == 1, A.b, nb)};
+}
+
+// ---- Frobenius (quad_frob_lane): a_k -> conj(a_k) gamma_k, with the
+// partner components Ap of A
+TBG_HD Fp2o hx_conj_view(uint32_t c, const Fp& own, const Fp& par) {
+  const Fp no = fp_reduce(fp_neg(own)), np = fp_reduce(fp_neg(par));
+  return {fp_select(c != 0, no, own), fp_select(c != 0, par, np)};  // conj(x) = (x0, -x1)
+}
+TBG_HD Fp2o hx_const_view(uint32_t c, const Fp2& k) { return {fp_select(c != 0, k.c1, k.c0), fp_select(c != 0, k.c0, k.c1)}; }
+TBG_HD Fp4h hx_frob(uint32_t c, int q, const Fp4h& A, const Fp4h& Ap) {
+  const Fp2 ga = fp2_select(q == 0, fp2_one(), fp2_select(q == 1, fp2_from_const(FROB_G1), fp2_from_const(FROB_G2)));
+  const Fp2 gb = fp2_select(q == 0, fp2_from_const(FROB_G3),
+                            fp2_select(q == 1, fp2_from_const(FROB_G4), fp2_from_const(FROB_G5)));
+  return {hx_mul(c, hx_conj_view(c, A.a, Ap.a), hx_const_view(c, ga)),
+          hx_mul(c, hx_conj_view(c, A.b, Ap.b), hx_const_view(c, gb))};
+}
+
+// this lane's part of "the element is 1": b = 0, a = 1 on (q, c) = (0, 0), 0 elsewhere
+TBG_HD bool hx_is_one_lane(uint32_t c, int q, const Fp4h& A) {
+  const bool a_one = fp_eq(A.a, fp_one()), a_zero = fp_is_zero(A.a);
+  return fp_is_zero(A.b) && ((q == 0 && c == 0) ? a_one : a_zero);
 }
 
 }  // namespace tbg
@@ -118,19 +177,35 @@ TBG_HD Fp4h hx_line2(uint32_t c, int q, const HxLine& r, const Fp& Wp) {
 #if defined(__HIP__)
 namespace tbg {
 
+// Where the component partner sits.  TBG_HEX_SWIZZLE = 1 (default): rows 0 / 1
+// (and 2 / 3) of the wave hold components 0 / 1 of the same five trios, the
+// partner is lane ^ 16, and the exchange is ONE ds_swizzle (the LDS crossbar
+// in xor mode, no LDS memory) per word.  0: halves of the wave, partner lane
+// ^ 32 by v_permlane32_swap -- which swaps between two registers, so every
+// word also took a copy and a per-half select (3 VALU instructions; 364
+// permlanes in k_miller_hex's loop body, profiles/r04).
+#ifndef TBG_HEX_SWIZZLE
+#define TBG_HEX_SWIZZLE 1
+#endif
 // Fp12 slot of global thread t (UINT32_MAX for lane 15 of a row), and the
 // threads n slots need: 10 per wave.
 TBG_HD inline uint32_t hex_slot(uint32_t t) {
   const uint32_t l = t & 15u;
-  return l == 15u ? 0xFFFFFFFFu : (t >> 6) * 10u + ((t >> 4) & 1u) * 5u + l / 3u;
+  const uint32_t set = TBG_HEX_SWIZZLE ? (t >> 5) & 1u : (t >> 4) & 1u;  // which five trios
+  return l == 15u ? 0xFFFFFFFFu : (t >> 6) * 10u + set * 5u + l / 3u;
 }
 inline uint32_t hex_threads(uint32_t n) { return 64u * ((n + 9u) / 10u); }
-TBG_DEV uint32_t hex_c() { return (threadIdx.x >> 5) & 1u; }
+TBG_DEV uint32_t hex_c() { return TBG_HEX_SWIZZLE ? (threadIdx.x >> 4) & 1u : (threadIdx.x >> 5) & 1u; }
 
-// the partner lane's (lane ^ 32) value
+// the partner lane's value
 TBG_DEV uint32_t hx_swap_u32(uint32_t v) {
+#if TBG_HEX_SWIZZLE
+  // bitmask mode within 32-lane groups: and 0x1f, or 0, xor 0x10 -> lane ^ 16
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+#else
   const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
   return (threadIdx.x & 32u) ? r[0] : r[1];
+#endif
 }
 TBG_DEV Fp hx_swap(const Fp& x) {
   Fp r;
@@ -218,6 +293,101 @@ TBG_DEV Fp4h hex_line_folded(const Fp4h& A, const uint32_t* lines, int idx) {
       l[k].p.l[i] = src[(2 * k + (int)(c ^ 1u)) * NL + i];
     }
   return hex_line_mul(A, nullptr, l[0], l[1], l[2]);
+}
+
+// x y (quad_mul_in on the hexad)
+TBG_DEV Fp4h hex_mul(const Fp4h& A, const Fp4h& B) {
+  const uint32_t c = hex_c();
+  const int q = quad_lane();
+  Fp t0, t1, s;
+  hx_mul1(c, hx_own_par(A, hx_swap(A)), hx_own_par(B, hx_swap(B)), t0, t1, s);
+  const Fp4h P = hx_mul2(c, t0, t1, hx_swap(t1), s);
+  const Fp4h SA = {fp_add(xch<QP_NEXT>(A.a), xch<QP_PREV>(A.a)), fp_add(xch<QP_NEXT>(A.b), xch<QP_PREV>(A.b))};
+  const Fp4h SB = {fp_add(xch<QP_NEXT>(B.a), xch<QP_PREV>(B.a)), fp_add(xch<QP_NEXT>(B.b), xch<QP_PREV>(B.b))};
+  hx_mul1(c, hx_own_par(SA, hx_swap(SA)), hx_own_par(SB, hx_swap(SB)), t0, t1, s);
+  const Fp4h Q = hx_mul2(c, t0, t1, hx_swap(t1), s);
+  const Fp4h Pn = hxch<QP_NEXT>(P), Pp = hxch<QP_PREV>(P), Qx = hxch<QP_SW12>(Q);
+  Fp4h T;
+  Fp V;
+  hx_comb1(q, P, Pn, Pp, Qx, T, V);
+  return hx_comb2(c, q, P, Pn, Pp, T, V, hx_swap(V));
+}
+
+// cyclotomic squaring (quad_cyc_sqr_in on the hexad)
+TBG_DEV Fp4h hex_cyc_sqr(const Fp4h& A) {
+  const uint32_t c = hex_c();
+  Fp ab, s;
+  hx_sqr1(c, hx_own_par(A, hx_swap(A)), ab, s);
+  const Fp4h T = hx_sqr2(c, ab, hx_swap(ab), s);
+  const Fp4h Tx = hxch<QP_SW12>(T);
+  return hx_cyc(c, quad_lane(), A, Tx, hx_swap(Tx.b));
+}
+
+TBG_DEV Fp4h hex_conj(const Fp4h& A) { return hx_conj(quad_lane(), A); }
+TBG_DEV Fp4h hex_frob(const Fp4h& A) { return hx_frob(hex_c(), quad_lane(), A, hx_swap(A)); }
+
+// true on all six lanes iff the hexad's element is 1
+TBG_DEV bool hex_is_one(const Fp4h& A) {
+  uint32_t v = hx_is_one_lane(hex_c(), quad_lane(), A) ? 1u : 0u;
+  v &= hx_swap_u32(v);
+  return (xch_u32<QP_B0>(v) & xch_u32<QP_B1>(v) & xch_u32<QP_B2>(v)) != 0;
+}
+
+// f^-1: the whole element gathered on every lane, the tower inverse, this
+// lane's components back (rare: once per final exponentiation)
+TBG_DEV Fp4h hex_inv(const Fp4h& A) {
+  const uint32_t c = hex_c();
+  const Fp4h Ap = hx_swap(A);
+  // this lane's view -> trio lane q's whole Fp4 (components 0 and 1)
+  auto whole = [&](const Fp4h& own, const Fp4h& par) -> Fp4 {
+    return {{fp_select(c != 0, par.a, own.a), fp_select(c != 0, own.a, par.a)},
+            {fp_select(c != 0, par.b, own.b), fp_select(c != 0, own.b, par.b)}};
+  };
+  const Fp4 A0 = whole(hxch<QP_B0>(A), hxch<QP_B0>(Ap)), A1 = whole(hxch<QP_B1>(A), hxch<QP_B1>(Ap)),
+            A2 = whole(hxch<QP_B2>(A), hxch<QP_B2>(Ap));
+  const Fp4 r = quad_from_fp12(quad_lane(), fp12_inv(quad_to_fp12(A0, A1, A2)));
+  return {fp_select(c != 0, r.a.c1, r.a.c0), fp_select(c != 0, r.b.c1, r.b.c0)};
+}
+
+// a^|x| in the cyclotomic subgroup, and the final exponentiation f^(3 (p^12
+// - 1) / r) in quad_final_exp's sequence (kernel-inline squarings; the rare
+// products, inversions and Frobenius maps stay calls)
+__device__ __noinline__ Fp4h hex_mul_ni(const Fp4h& A, const Fp4h& B) { return hex_mul(A, B); }
+__device__ __noinline__ Fp4h hex_frob_ni(const Fp4h& A) { return hex_frob(A); }
+__device__ __noinline__ Fp4h hex_inv_ni(const Fp4h& A) { return hex_inv(A); }
+TBG_DEV Fp4h hex_pow_xabs_in(const Fp4h& a) {
+  Fp4h r = a;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    r = hex_cyc_sqr(r);
+    if ((X_ABS >> i) & 1) r = hex_mul_ni(r, a);
+  }
+  return r;
+}
+TBG_DEV Fp4h hex_pow_x_in(const Fp4h& a) { return hex_conj(hex_pow_xabs_in(a)); }
+TBG_DEV Fp4h hex_final_exp_in(const Fp4h& f) {
+  Fp4h t = hex_mul_ni(hex_conj(f), hex_inv_ni(f));
+  t = hex_mul_ni(hex_frob_ni(hex_frob_ni(t)), t);
+  Fp4h a = hex_mul_ni(hex_pow_x_in(t), hex_conj(t));
+  a = hex_mul_ni(hex_pow_x_in(a), hex_conj(a));
+  Fp4h b = hex_mul_ni(hex_pow_x_in(a), hex_frob_ni(a));
+  Fp4h c = hex_mul_ni(hex_pow_x_in(hex_pow_x_in(b)), hex_frob_ni(hex_frob_ni(b)));
+  c = hex_mul_ni(c, hex_conj(b));
+  Fp4h t3 = hex_mul_ni(hex_cyc_sqr(t), t);
+  return hex_mul_ni(c, t3);
+}
+
+// quad layout in HBM, read: lane (q, c) loads its two components
+TBG_DEV Fp4h hex_load(const uint32_t* src) {
+  const int q = quad_lane();
+  const uint32_t c = hex_c();
+  Fp4h A;
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    A.a.l[j] = src[4 * NL * q + c * NL + j];
+    A.b.l[j] = src[4 * NL * q + (2 + c) * NL + j];
+  }
+  return A;
 }
 
 // quad layout in HBM (bls_quad.h / k_rlc.hip QUAD_WORDS = 4 NL per trio

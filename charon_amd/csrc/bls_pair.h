@@ -35,9 +35,11 @@ TBG_HD Fp pair_mul_lane(uint32_t par, const Fp& a, const Fp& ap, const Fp& b, co
   const Fp nbp = fp_neg(bp);
   return fp_mul2(a, fp_select(par != 0, bp, b), ap, fp_select(par != 0, b, nbp));
 }
+// (the lane's operands a, a' normalised: a' is subtracted; the two factors
+// stay lazy, fp_mul's columns take their limbs)
 TBG_HD Fp pair_sqr_lane(uint32_t par, const Fp& a, const Fp& ap) {
-  const Fp x = fp_add(fp_select(par != 0, ap, a), ap);       // even a + a', odd 2 a'
-  const Fp y = fp_select(par != 0, a, fp_sub(a, ap));        // even a - a', odd a
+  const Fp x = fp_add_l(fp_select(par != 0, ap, a), ap);     // even a + a', odd 2 a'
+  const Fp y = fp_select(par != 0, a, fp_sub_l(a, ap));      // even a - a', odd a
   return fp_mul(x, y);
 }
 TBG_HD Fp pair_conj_lane(uint32_t par, const Fp& a) { return fp_select(par != 0, fp_neg(a), a); }
@@ -55,6 +57,8 @@ TBG_HD Fp pair_const(uint32_t par, const Fp2Const& c) { return par ? fp_from_con
 struct Fp2p { Fp c0, c1; };
 TBG_HD Fp2p f_add(const Fp2p& a, const Fp2p& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
 TBG_HD Fp2p f_sub(const Fp2p& a, const Fp2p& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+TBG_HD Fp2p f_add_l(const Fp2p& a, const Fp2p& b) { return {fp_add_l(a.c0, b.c0), fp_add_l(a.c1, b.c1)}; }
+TBG_HD Fp2p f_sub_l(const Fp2p& a, const Fp2p& b) { return {fp_sub_l(a.c0, b.c0), fp_sub_l(a.c1, b.c1)}; }
 TBG_HD Fp2p f_neg(const Fp2p& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
 TBG_HD Fp2p f_reduce(const Fp2p& a) { return {fp_reduce(a.c0), fp_reduce(a.c1)}; }
 TBG_HD Fp2p f_small(const Fp2p& a, uint32_t k) { return {fp_mul_small(a.c0, k), fp_mul_small(a.c1, k)}; }
@@ -100,10 +104,10 @@ TBG_HD Jac<F> jac_add_x(const Jac<F>& p, const Jac<F>& q, bool& exc) {
   const F Z2Z2 = f_sqr(q.Z);
   const F S1 = f_mul(f_mul(p.Y, q.Z), Z2Z2);
   const F S2 = f_mul(f_mul(q.Y, p.Z), Z1Z1);
-  const F Zs = f_reduce(f_sub(f_sqr(f_add(p.Z, q.Z)), f_add(Z1Z1, Z2Z2)));
+  const F Zs = f_reduce(f_sub_l(f_sqr(f_add(p.Z, q.Z)), f_add(Z1Z1, Z2Z2)));
   const F U1 = f_mul(p.X, Z2Z2);
-  const F H = f_reduce(f_sub(f_mul(q.X, Z1Z1), U1));
-  const F Rr = f_reduce(f_sub(S2, S1));
+  const F H = f_reduce(f_sub_l(f_mul(q.X, Z1Z1), U1));
+  const F Rr = f_reduce(f_sub_l(S2, S1));
   if (f_is_zero(H)) {
     if (f_is_zero(Rr)) exc = true;
     return jac_inf<F>();
@@ -114,8 +118,8 @@ TBG_HD Jac<F> jac_add_x(const Jac<F>& p, const Jac<F>& q, bool& exc) {
   const F J = f_mul(H, I);
   const F V = f_mul(U1, I);
   const F r2 = f_add(Rr, Rr);
-  const F X3 = f_reduce(f_sub(f_sub(f_sqr(r2), J), f_add(V, V)));
-  const F Y3 = f_reduce(f_sub(f_mul(f_sub(V, X3), r2), f_small(f_mul(S1, J), 2)));
+  const F X3 = f_reduce(f_sub_l(f_sub_l(f_sqr(r2), J), f_add(V, V)));
+  const F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(V, X3), r2), f_small(f_mul(S1, J), 2)));
   return {X3, Y3, Z3};
 }
 
@@ -123,15 +127,15 @@ TBG_HD Jac<F> jac_add_x(const Jac<F>& p, const Jac<F>& q, bool& exc) {
 template <class F>
 TBG_HD Jac<F> jac_dbl_lo(const Jac<F>& p) {
   const F YZ = f_mul(p.Y, p.Z);
-  const F Z3 = f_reduce(f_add(YZ, YZ));
+  const F Z3 = f_reduce(f_add_l(YZ, YZ));
   const F B = f_sqr(p.Y);
   const F A = f_sqr(p.X);
   const F C = f_sqr(B);
-  const F t = f_sub(f_sqr(f_add(p.X, B)), f_add(A, C));   // < 18p
-  const F D = f_reduce(f_add(t, t));
+  const F t = f_sub_l(f_sqr(f_add(p.X, B)), f_add(A, C));   // < 18p
+  const F D = f_reduce(f_add_l(t, t));
   const F E = f_small(A, 3);                                // < 6p
-  const F X3 = f_reduce(f_sub(f_sqr(E), f_add(D, D)));
-  const F Y3 = f_reduce(f_sub(f_mul(f_sub(D, X3), E), f_small(C, 8)));
+  const F X3 = f_reduce(f_sub_l(f_sqr(E), f_add(D, D)));
+  const F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(D, X3), E), f_small(C, 8)));
   return {X3, Y3, Z3};
 }
 
@@ -142,8 +146,8 @@ TBG_HD Jac<F> jac_add_aff_x(const Jac<F>& p, const Aff<F>& q, bool& exc) {
   F Z1Z1 = f_sqr(p.Z);
   F U2 = f_mul(q.x, Z1Z1);
   F S2 = f_mul(f_mul(q.y, p.Z), Z1Z1);
-  F H = f_reduce(f_sub(U2, p.X));
-  F Rr = f_reduce(f_sub(S2, p.Y));
+  F H = f_reduce(f_sub_l(U2, p.X));
+  F Rr = f_reduce(f_sub_l(S2, p.Y));
   if (f_is_zero(H)) {
     if (f_is_zero(Rr)) exc = true;
     return jac_inf<F>();
@@ -153,9 +157,9 @@ TBG_HD Jac<F> jac_add_aff_x(const Jac<F>& p, const Aff<F>& q, bool& exc) {
   F J = f_mul(H, I);
   F r2 = f_add(Rr, Rr);
   F V = f_mul(p.X, I);
-  F X3 = f_reduce(f_sub(f_sub(f_sqr(r2), J), f_add(V, V)));
-  F Y3 = f_reduce(f_sub(f_mul(f_sub(V, X3), r2), f_small(f_mul(p.Y, J), 2)));
-  F Z3 = f_reduce(f_sub(f_sub(f_sqr(f_add(p.Z, H)), Z1Z1), HH));
+  F X3 = f_reduce(f_sub_l(f_sub_l(f_sqr(r2), J), f_add(V, V)));
+  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(V, X3), r2), f_small(f_mul(p.Y, J), 2)));
+  F Z3 = f_reduce(f_sub_l(f_sub_l(f_sqr(f_add(p.Z, H)), Z1Z1), HH));
   return {X3, Y3, Z3};
 }
 
@@ -210,16 +214,16 @@ TBG_HD LineG<F> miller_dbl_g(Jac<F>& T, const Fp& nxP, const Fp& yP) {
   F B = f_sqr(T.Y);
   F C = f_sqr(B);
   F ZZ = f_sqr(T.Z);
-  F t = f_sub(f_sqr(f_add(T.X, B)), f_add(A, C));
-  F D = f_reduce(f_add(t, t));
+  F t = f_sub_l(f_sqr(f_add(T.X, B)), f_add(A, C));
+  F D = f_reduce(f_add_l(t, t));
   F E = f_small(A, 3);
   F Fv = f_sqr(E);
-  F X3 = f_reduce(f_sub(Fv, f_add(D, D)));
-  F Y3 = f_reduce(f_sub(f_mul(f_sub(D, X3), E), f_small(C, 8)));
+  F X3 = f_reduce(f_sub_l(Fv, f_add(D, D)));
+  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(D, X3), E), f_small(C, 8)));
   F YZ = f_mul(T.Y, T.Z);
-  F Z3 = f_reduce(f_add(YZ, YZ));
+  F Z3 = f_reduce(f_add_l(YZ, YZ));
   LineG<F> l;
-  l.l0 = f_reduce(f_sub(f_mul(T.X, E), f_add(B, B)));   // 3X^3 - 2Y^2
+  l.l0 = f_reduce(f_sub_l(f_mul(T.X, E), f_add(B, B)));   // 3X^3 - 2Y^2
   l.l1 = f_mulfp(f_mul(ZZ, E), nxP);                     // -3X^2 Z^2 xP
   l.l4 = f_mulfp(f_mul(Z3, ZZ), yP);                     // 2 Y Z^3 yP
   T = {X3, Y3, Z3};
@@ -231,16 +235,16 @@ TBG_HD LineG<F> miller_add_g(Jac<F>& T, const Aff<F>& Q, const Fp& nxP, const Fp
   F ZZ = f_sqr(T.Z);
   F U2 = f_mul(Q.x, ZZ);
   F S2 = f_mul(f_mul(Q.y, T.Z), ZZ);
-  F H = f_reduce(f_sub(U2, T.X));
-  F R = f_reduce(f_sub(S2, T.Y));
+  F H = f_reduce(f_sub_l(U2, T.X));
+  F R = f_reduce(f_sub_l(S2, T.Y));
   F HH = f_sqr(H);
   F HHH = f_mul(H, HH);
   F V = f_mul(T.X, HH);
-  F X3 = f_reduce(f_sub(f_sub(f_sqr(R), HHH), f_add(V, V)));
-  F Y3 = f_reduce(f_sub(f_mul(f_sub(V, X3), R), f_mul(T.Y, HHH)));
+  F X3 = f_reduce(f_sub_l(f_sub_l(f_sqr(R), HHH), f_add(V, V)));
+  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(V, X3), R), f_mul(T.Y, HHH)));
   F Z3 = f_mul(T.Z, H);
   LineG<F> l;
-  l.l0 = f_reduce(f_sub(f_mul(R, Q.x), f_mul(Q.y, Z3)));
+  l.l0 = f_reduce(f_sub_l(f_mul(R, Q.x), f_mul(Q.y, Z3)));
   l.l1 = f_mulfp(R, nxP);
   l.l4 = f_mulfp(Z3, yP);
   T = {X3, Y3, Z3};
@@ -282,7 +286,8 @@ constexpr int QP_PAIR = 1 | (0 << 2) | (3 << 4) | (2 << 6);  // quad_perm [1, 0,
 
 TBG_DEV uint32_t pair_par() { return threadIdx.x & 1u; }
 TBG_DEV uint32_t pair_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, QP_PAIR, 0xf, 0xf, false);
+  // (every lane's source is valid; bound_ctrl spares the v_mov of `old`)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, QP_PAIR, 0xf, 0xf, true);
 }
 TBG_DEV Fp pair_xch(const Fp& x) {
   Fp r;
@@ -298,6 +303,8 @@ TBG_DEV bool pair_all(bool b) {
 
 TBG_DEV Fp2x f_add(const Fp2x& a, const Fp2x& b) { return {fp_add(a.v, b.v)}; }
 TBG_DEV Fp2x f_sub(const Fp2x& a, const Fp2x& b) { return {fp_sub(a.v, b.v)}; }
+TBG_DEV Fp2x f_add_l(const Fp2x& a, const Fp2x& b) { return {fp_add_l(a.v, b.v)}; }
+TBG_DEV Fp2x f_sub_l(const Fp2x& a, const Fp2x& b) { return {fp_sub_l(a.v, b.v)}; }
 TBG_DEV Fp2x f_neg(const Fp2x& a) { return {fp_neg(a.v)}; }
 TBG_DEV Fp2x f_reduce(const Fp2x& a) { return {fp_reduce(a.v)}; }
 TBG_DEV Fp2x f_small(const Fp2x& a, uint32_t k) { return {fp_mul_small(a.v, k)}; }

@@ -23,6 +23,8 @@ struct Fp4 { Fp2 a, b; };  // a + b y, y^2 = xi
 TBG_HD Fp4 fp4_add(const Fp4& x, const Fp4& y) { return {fp2_add(x.a, y.a), fp2_add(x.b, y.b)}; }
 TBG_HD Fp4 fp4_sub(const Fp4& x, const Fp4& y) { return {fp2_sub(x.a, y.a), fp2_sub(x.b, y.b)}; }
 TBG_HD Fp4 fp4_reduce(const Fp4& x) { return {fp2_reduce(x.a), fp2_reduce(x.b)}; }
+TBG_HD Fp4 fp4_add_l(const Fp4& x, const Fp4& y) { return {fp2_add_l(x.a, y.a), fp2_add_l(x.b, y.b)}; }
+TBG_HD Fp4 fp4_sub_l(const Fp4& x, const Fp4& y) { return {fp2_sub_l(x.a, y.a), fp2_sub_l(x.b, y.b)}; }
 TBG_HD Fp4 fp4_select(bool c, const Fp4& x, const Fp4& y) { return {fp2_select(c, x.a, y.a), fp2_select(c, x.b, y.b)}; }
 TBG_HD Fp4 fp4_zero() { return {fp2_zero(), fp2_zero()}; }
 // x * y (the Fp4 generator): (a + b y) y = xi b + a y   [lazy]
@@ -32,9 +34,9 @@ TBG_HD Fp4 fp4_mul_y(const Fp4& x) { return {fp2_mul_xi(x.b), x.a}; }
 TBG_HD Fp4 fp4_mul(const Fp4& x, const Fp4& y) {
   Fp2 t0 = fp2_mul(x.a, y.a);
   Fp2 t1 = fp2_mul(x.b, y.b);
-  Fp2 s = fp2_mul(fp2_add(x.a, x.b), fp2_add(y.a, y.b));
-  Fp2 c0 = fp2_reduce(fp2_add(t0, fp2_mul_xi(t1)));
-  Fp2 c1 = fp2_reduce(fp2_sub(s, fp2_add(t0, t1)));
+  Fp2 s = fp2_mul(fp2_add_l(x.a, x.b), fp2_add(y.a, y.b));
+  Fp2 c0 = fp2_reduce(fp2_add_l(fp2_mul_xi(t1), t0));
+  Fp2 c1 = fp2_reduce(fp2_sub_l(s, fp2_add(t0, t1)));
   return {c0, c1};
 }
 
@@ -55,11 +57,11 @@ TBG_HD Fp4 fp4_mul_fp2(const Fp4& x, const Fp2& s) { return {fp2_mul(x.a, s), fp
 TBG_HD Fp4 quad_combine(int q, const Fp4& P, const Fp4& Pn, const Fp4& Pp, const Fp4& Qx) {
   Fp4 f1 = fp4_select(q == 1, Pp, Pn);
   Fp4 f2 = fp4_select(q == 0, Pp, P);
-  Fp4 T = fp4_reduce(fp4_sub(Qx, fp4_add(f1, f2)));           // < 2p
+  Fp4 T = fp4_reduce(fp4_sub_l(Qx, fp4_add(f1, f2)));           // < 2p
   Fp4 yPn = fp4_reduce(fp4_mul_y(Pn));
   Fp4 W = fp4_select(q == 0, P, fp4_select(q == 1, yPn, Pp));
   Fp4 Ty = fp4_reduce(fp4_mul_y(T));
-  return fp4_reduce(fp4_add(fp4_select(q == 0, Ty, T), W));
+  return fp4_reduce(fp4_add_l(fp4_select(q == 0, Ty, T), W));
 }
 
 // Line f * (L0 + L2 x^2), L0 = (l0, l4), L2 = l1 (in Fp2):
@@ -68,7 +70,7 @@ TBG_HD Fp4 quad_line_lane(int q, const Fp4& A, const Fp4& An, const Fp2& l0, con
   Fp4 t = fp4_mul(A, {l0, l4});
   Fp4 u = fp4_mul_fp2(An, l1);
   Fp4 uy = fp4_reduce(fp4_mul_y(u));
-  return fp4_reduce(fp4_add(t, fp4_select(q < 2, uy, u)));
+  return fp4_reduce(fp4_add_l(t, fp4_select(q < 2, uy, u)));
 }
 
 // Cyclotomic squaring (Granger-Scott) per lane: T = fp4_sqr(A_q) on every
@@ -78,8 +80,8 @@ TBG_HD Fp4 quad_cyc_lane(int q, const Fp4& A, const Fp4& Tx) {
   Fp2 s2 = fp2_select(q == 1, Tx.a, Tx.b);
   Fp2 a2 = fp2_dbl(A.a), b2 = fp2_dbl(A.b);
   Fp2 s13 = fp2_mul_small(s1, 3), s23 = fp2_mul_small(s2, 3);
-  Fp2 na = fp2_select(q == 1, fp2_add(s13, a2), fp2_sub(s13, a2));
-  Fp2 nb = fp2_select(q == 1, fp2_sub(s23, b2), fp2_add(s23, b2));
+  Fp2 na = fp2_select(q == 1, fp2_add_l(s13, a2), fp2_sub_l(s13, a2));
+  Fp2 nb = fp2_select(q == 1, fp2_sub_l(s23, b2), fp2_add_l(s23, b2));
   return {fp2_reduce(na), fp2_reduce(nb)};
 }
 
@@ -145,9 +147,12 @@ enum QuadXch : int {
   QP_B2 = 5,    // 2
 };
 
+// bound_ctrl: a lane whose source is outside its row reads 0 -- the value the
+// `old` operand gave before, but without the v_mov that initialised it for
+// every exchanged word (532 of k_miller_hex's loop-body instructions)
 template <int CTRL>
 TBG_DEV uint32_t dpp_u32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
 }
 
 #if TBG_TRIO

@@ -31,6 +31,9 @@ TBG_HD Fp2 fp2_reduce(const Fp2& a) { return {fp_reduce(a.c0), fp_reduce(a.c1)};
 TBG_HD Fp2 fp2_canon(const Fp2& a) { return {fp_canon(a.c0), fp_canon(a.c1)}; }
 TBG_HD Fp2 fp2_select(bool c, const Fp2& a, const Fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
 TBG_HD Fp2 fp2_mul_small(const Fp2& a, uint32_t k) { return {fp_mul_small(a.c0, k), fp_mul_small(a.c1, k)}; }
+// lazy limbs (bls_field.h): results for reductions and first operands only
+TBG_HD Fp2 fp2_add_l(const Fp2& a, const Fp2& b) { return {fp_add_l(a.c0, b.c0), fp_add_l(a.c1, b.c1)}; }
+TBG_HD Fp2 fp2_sub_l(const Fp2& a, const Fp2& b) { return {fp_sub_l(a.c0, b.c0), fp_sub_l(a.c1, b.c1)}; }
 
 // Fp2 product.  TBG_FP2_KARA=1: Karatsuba with lazy reduction —
 // the three half products a0*b0, a1*b1, (a0+a1)(b0+b1) are scanned column by
@@ -116,16 +119,18 @@ TBG_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
 #endif
 
 TBG_HD Fp2 fp2_sqr(const Fp2& a) {
-  Fp s = fp_add(a.c0, a.c1);
-  Fp d = fp_sub(a.c0, a.c1);
-  Fp a0d = fp_dbl(a.c0);
+  Fp s = fp_add_l(a.c0, a.c1);
+  Fp d = fp_sub_l(a.c0, a.c1);
+  Fp a0d = fp_add_l(a.c0, a.c0);
   return {fp_mul(s, d), fp_mul(a0d, a.c1)};
 }
 
 TBG_HD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return {fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
 
-// (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u   [lazy: c0 < a0 + 16p, c1 < a0 + a1]
-TBG_HD Fp2 fp2_mul_xi(const Fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+// (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u   [lazy: c0 < a0 + 16p, c1 < a0 + a1;
+// lazy limbs too: every use reduces it, adds it to something that is
+// reduced or normalised, or subtracts from it]
+TBG_HD Fp2 fp2_mul_xi(const Fp2& a) { return {fp_sub_l(a.c0, a.c1), fp_add_l(a.c0, a.c1)}; }
 
 TBG_HD bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
 TBG_HD bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
@@ -216,13 +221,13 @@ TBG_NI Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
   Fp2 t0 = fp2_mul(a.c0, b.c0);
   Fp2 t1 = fp2_mul(a.c1, b.c1);
   Fp2 t2 = fp2_mul(a.c2, b.c2);
-  Fp2 s12 = fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2));
-  Fp2 s01 = fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1));
-  Fp2 s02 = fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2));
-  Fp2 u = fp2_reduce(fp2_sub(s12, fp2_add(t1, t2)));         // < 2p
-  Fp2 c0 = fp2_reduce(fp2_add(t0, fp2_mul_xi(u)));             // t0 + xi(s12 - t1 - t2)
-  Fp2 c1 = fp2_reduce(fp2_add(fp2_sub(s01, fp2_add(t0, t1)), fp2_mul_xi(t2)));
-  Fp2 c2 = fp2_reduce(fp2_add(fp2_sub(s02, fp2_add(t0, t2)), t1));
+  Fp2 s12 = fp2_mul(fp2_add_l(a.c1, a.c2), fp2_add(b.c1, b.c2));
+  Fp2 s01 = fp2_mul(fp2_add_l(a.c0, a.c1), fp2_add(b.c0, b.c1));
+  Fp2 s02 = fp2_mul(fp2_add_l(a.c0, a.c2), fp2_add(b.c0, b.c2));
+  Fp2 u = fp2_reduce(fp2_sub_l(s12, fp2_add(t1, t2)));         // < 2p
+  Fp2 c0 = fp2_reduce(fp2_add_l(fp2_mul_xi(u), t0));             // t0 + xi(s12 - t1 - t2)
+  Fp2 c1 = fp2_reduce(fp2_add_l(fp2_sub_l(s01, fp2_add(t0, t1)), fp2_mul_xi(t2)));
+  Fp2 c2 = fp2_reduce(fp2_add_l(fp2_sub_l(s02, fp2_add(t0, t2)), t1));
   return {c0, c1, c2};
 }
 
@@ -232,12 +237,12 @@ TBG_HD Fp6 fp6_sqr(const Fp6& a) { return fp6_mul(a, a); }
 TBG_HD Fp6 fp6_mul_by_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
   Fp2 t0 = fp2_mul(a.c0, b0);
   Fp2 t1 = fp2_mul(a.c1, b1);
-  Fp2 s01 = fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1));
+  Fp2 s01 = fp2_mul(fp2_add_l(a.c0, a.c1), fp2_add(b0, b1));
   Fp2 a2b1 = fp2_mul(a.c2, b1);
   Fp2 a2b0 = fp2_mul(a.c2, b0);
-  Fp2 c0 = fp2_reduce(fp2_add(t0, fp2_mul_xi(a2b1)));
-  Fp2 c1 = fp2_reduce(fp2_sub(s01, fp2_add(t0, t1)));
-  Fp2 c2 = fp2_reduce(fp2_add(t1, a2b0));
+  Fp2 c0 = fp2_reduce(fp2_add_l(fp2_mul_xi(a2b1), t0));
+  Fp2 c1 = fp2_reduce(fp2_sub_l(s01, fp2_add(t0, t1)));
+  Fp2 c2 = fp2_reduce(fp2_add_l(t1, a2b0));
   return {c0, c1, c2};
 }
 

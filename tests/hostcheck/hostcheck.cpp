@@ -339,6 +339,121 @@ static Q3 final_exp(const Q3& f) {
 }
 }  // namespace qe
 
+// The hexad's final-exponentiation pieces (hex_mul, hex_cyc_sqr, hex_frob,
+// hex_conj, hex_inv, hex_final_exp_in) emulated lane by lane: H6.v[q][c] is
+// what lane (q, c) holds, c ^ 1 the ds_swizzle partner.
+namespace he {
+struct H6 { Fp4h v[3][2]; };
+static H6 split(const Fp12& f) {
+  Fp4 A[3];
+  q_split(f, A);
+  H6 r;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) r.v[q][c] = {c ? A[q].a.c1 : A[q].a.c0, c ? A[q].b.c1 : A[q].b.c0};
+  return r;
+}
+static Fp12 join(const H6& h) { return hx_join(h.v); }
+static Fp4o own_par(const H6& h, int q, uint32_t c) {
+  return {{h.v[q][c].a, h.v[q][c ^ 1].a}, {h.v[q][c].b, h.v[q][c ^ 1].b}};
+}
+static H6 sum_others(const H6& h) {
+  H6 r;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c)
+      r.v[q][c] = {fp_add(h.v[(q + 1) % 3][c].a, h.v[(q + 2) % 3][c].a),
+                   fp_add(h.v[(q + 1) % 3][c].b, h.v[(q + 2) % 3][c].b)};
+  return r;
+}
+static H6 fp4mul(const H6& A, const H6& B) {
+  Fp t0[3][2], t1[3][2], s[3][2];
+  H6 P;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) hx_mul1(c, own_par(A, q, c), own_par(B, q, c), t0[q][c], t1[q][c], s[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) P.v[q][c] = hx_mul2(c, t0[q][c], t1[q][c], t1[q][c ^ 1], s[q][c]);
+  return P;
+}
+static H6 fp4sqr(const H6& A) {
+  Fp ab[3][2], s[3][2];
+  H6 P;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) hx_sqr1(c, own_par(A, q, c), ab[q][c], s[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) P.v[q][c] = hx_sqr2(c, ab[q][c], ab[q][c ^ 1], s[q][c]);
+  return P;
+}
+static H6 combine(const H6& P, const H6& Q) {
+  Fp4h T[3][2];
+  Fp V[3][2];
+  H6 R;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c)
+      hx_comb1(q, P.v[q][c], P.v[(q + 1) % 3][c], P.v[(q + 2) % 3][c], Q.v[SW12[q]][c], T[q][c], V[q][c]);
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c)
+      R.v[q][c] = hx_comb2(c, q, P.v[q][c], P.v[(q + 1) % 3][c], P.v[(q + 2) % 3][c], T[q][c], V[q][c], V[q][c ^ 1]);
+  return R;
+}
+static H6 mul(const H6& A, const H6& B) { return combine(fp4mul(A, B), fp4mul(sum_others(A), sum_others(B))); }
+static H6 cyc(const H6& A) {
+  const H6 T = fp4sqr(A);
+  H6 R;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) R.v[q][c] = hx_cyc(c, q, A.v[q][c], T.v[SW12[q]][c], T.v[SW12[q]][c ^ 1].b);
+  return R;
+}
+static H6 conj(const H6& A) {
+  H6 R;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) R.v[q][c] = hx_conj(q, A.v[q][c]);
+  return R;
+}
+static H6 frob(const H6& A) {
+  H6 R;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) R.v[q][c] = hx_frob(c, q, A.v[q][c], A.v[q][c ^ 1]);
+  return R;
+}
+static H6 inv(const H6& A) { return split(fp12_inv(join(A))); }
+static bool is_one(const H6& A) {
+  bool ok = true;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) ok = ok && hx_is_one_lane(c, q, A.v[q][c]);
+  return ok;
+}
+static H6 pow_x(const H6& a) {
+  H6 r = a;
+  for (int i = 62; i >= 0; --i) { r = cyc(r); if ((X_ABS >> i) & 1) r = mul(r, a); }
+  return conj(r);
+}
+static H6 final_exp(const H6& f) {
+  H6 t = mul(conj(f), inv(f));
+  t = mul(frob(frob(t)), t);
+  H6 a = mul(pow_x(t), conj(t));
+  a = mul(pow_x(a), conj(a));
+  H6 b = mul(pow_x(a), frob(a));
+  H6 c = mul(pow_x(pow_x(b)), frob(frob(b)));
+  c = mul(c, conj(b));
+  H6 t3 = mul(cyc(t), t);
+  return mul(c, t3);
+}
+}  // namespace he
+
+extern "C" {
+void hc_hex_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  f12_out(he::join(he::mul(he::split(f12_in(a)), he::split(f12_in(b)))), out);
+}
+void hc_hex_cyc_sqr(const uint8_t* a, uint8_t* out) { f12_out(he::join(he::cyc(he::split(f12_in(a)))), out); }
+void hc_hex_frob(const uint8_t* a, uint8_t* out) { f12_out(he::join(he::frob(he::split(f12_in(a)))), out); }
+void hc_hex_conj(const uint8_t* a, uint8_t* out) { f12_out(he::join(he::conj(he::split(f12_in(a)))), out); }
+// the final exponentiation; returns whether the result is 1 by the lanes' test
+int hc_hex_final_exp(const uint8_t* a, uint8_t* out) {
+  const he::H6 r = he::final_exp(he::split(f12_in(a)));
+  f12_out(he::join(r), out);
+  return he::is_one(r) ? 1 : 0;
+}
+}
+
 extern "C" {
 static uint32_t g_sig_lines[LINES_WORDS], g_h_lines[LINES_WORDS];
 // stage 1: line precomputation for one partial (signature lines) and its message (H lines)
@@ -533,6 +648,33 @@ void hc_pair_ops(const uint8_t* a96, const uint8_t* b96, uint8_t* out) {
   f2_out_pp(f_reduce(pp_conj(a)), out + 288);
   f2_out_pp(f_reduce(pp_mul_xi(a)), out + 384);
   f2_out_pp(pp_mul_const(a, PSI_X), out + 480);
+}
+// k_lines_h (pair-emulated miller_dbl_g / miller_add_g) against the
+// single-lane g2_lines of the same point, and the pair-emulated cofactor
+// clearing (g2_clear_cofactor_g, k_hash_clear_*) against g2_clear_cofactor:
+// bit 1 lines equal, bit 2 clearing equal (or the doubling exception taken).
+int hc_pair_lines_clear(const uint8_t* sig96) {
+  G2A q;
+  if (g2_decompress_t<true, false>(sig96, q) != DEC_OK) return -1;  // (no subgroup check: E2 points too)
+  static uint32_t ref[LINES_WORDS];
+  const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X))), y = fp_from_const(G1_NEG_Y);
+  g2_lines(q, nx, y, ref);
+  Aff<Fp2p> Q{pp_from(q.x), pp_from(q.y)};
+  Jac<Fp2p> T = jac_from_aff(Q);
+  int idx = 0, out = 1;
+  auto same = [&](const LineG<Fp2p>& l) {
+    const Line r = line_load(ref + LINE_WORDS * idx++);
+    if (!fp2_eq(pp_to(l.l0), r.l0) || !fp2_eq(pp_to(l.l1), r.l1) || !fp2_eq(pp_to(l.l4), r.l4)) out = 0;
+  };
+  for (int i = 62; i >= 0; --i) {
+    same(miller_dbl_g(T, nx, y));
+    if ((X_ABS >> i) & 1) same(miller_add_g(T, Q, nx, y));
+  }
+  bool exc = false;
+  const Jac<Fp2p> c = g2_clear_cofactor_g(Jac<Fp2p>{Q.x, Q.y, f_one<Fp2p>()}, exc);
+  const G2J cg{pp_to(c.X), pp_to(c.Y), pp_to(c.Z)};
+  if (exc || jac_eq(cg, g2_clear_cofactor(jac_from_aff(q)))) out |= 2;
+  return out;
 }
 // k_decode_sigs + k_subgroup_sigs: decode without the subgroup check, then the
 // pair-emulated check; returns a DecodeStatus like g2_decompress.

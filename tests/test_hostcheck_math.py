@@ -377,6 +377,21 @@ def test_lane_pair_subgroup_check_matches_decode():
             assert L.hc_pair_decode_sig(bytes.fromhex(p["sig"])) == 0
 
 
+def test_lane_pair_lines_and_cofactor_clearing():
+    """k_lines_h and k_hash_clear_* (pair-emulated, lazy sums in the group
+    law) equal the single-lane lines and cofactor clearing; the bound checks
+    of the host build (limbs, 64-bit columns) hold along the way."""
+    import json
+    import os
+    L = lib()
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    sigs = [p["sig"] for v in json.load(open(os.path.join(gold, "cfg1_3of4_single.json")))["vectors"]
+            for p in v["partials"]]
+    pools = json.load(open(os.path.join(gold, "invalid_g2.json")))["pools"]
+    for h in sigs[:4] + pools["non_subgroup"][:2]:  # E2 points in and outside G2
+        assert L.hc_pair_lines_clear(bytes.fromhex(h)) == 3, h
+
+
 def test_level0_bucket_msm_matches_rlc_products():
     """Level 0's signature side (bls_msm.h, k_msm.hip): the bucket method over
     the signed base-x digits equals the sum of the per-partial RLC products,
@@ -435,6 +450,30 @@ def test_workgroup_batch_inversion_matches_per_value_inverse():
         got = [fe(out.raw[48 * i:48 * i + 48]) for i in range(n)]
         for v, pz, g in zip(vals, present, got):
             assert g == (pow(v, P - 2, P) if pz else 1)
+
+
+def test_hex_final_exp_pieces_match_tower():
+    """bls_hex.h final exponentiation on the hexad (the fallback-check kernels'
+    layout): product, cyclotomic squaring, Frobenius, conjugation and the
+    whole f^(3 (p^12 - 1) / r), the six lanes emulated phase by phase, equal
+    the oracle's tower; the lanes' is-one test agrees."""
+    a, b = rand_f12(), rand_f12()
+    assert b2f12(call("hc_hex_mul", f12b(a), f12b(b), out=576)) == bls.f12_mul(a, b)
+    assert b2f12(call("hc_hex_frob", f12b(a), out=576)) == bls.f12_frob_n(a, 1)
+    assert b2f12(call("hc_hex_conj", f12b(a), out=576)) == bls.f12_conj(a)
+    f = bls.f12_mul(bls.f12_conj(a), bls.f12_inv(a))
+    f = bls.f12_mul(bls.f12_frob_n(f, 2), f)
+    assert b2f12(call("hc_hex_cyc_sqr", f12b(f), out=576)) == bls.f12_sqr(f)
+    import ctypes
+    out = ctypes.create_string_buffer(576)
+    one = lib().hc_hex_final_exp(f12b(a), out)
+    assert b2f12(out.raw) == bls.final_exp(a) and one == 0
+    # a product of pairings that cancels: e(P, Q) e(-P, Q) before the final exponentiation
+    p = bls.g1_mul(bls.G1_GEN, rng.randrange(1, bls.R))
+    q = bls.g2_mul(bls.G2_GEN, rng.randrange(1, bls.R))
+    m1 = b2f12(call("hc_miller", be(p[0]) + be(p[1]), aff2b(q), out=576))
+    m2 = b2f12(call("hc_miller", be(p[0]) + be((P - p[1]) % P), aff2b(q), out=576))
+    assert lib().hc_hex_final_exp(f12b(bls.f12_mul(m1, m2)), out) == 1
 
 
 def test_wide_fp12_final_exp_matches_oracle():
