@@ -120,7 +120,7 @@ STAGE_KERNELS = {
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
                 "k_lines_fold<FOLD_L0>", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>"],
     "h_lines": ["k_lines_h"],
-    "verify": ["k_miller_hex<MILLER_L0>", "k_miller_hex<MILLER_GROUPS>", "k_miller_hex<MILLER_GROUP_S>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_after",
+    "verify": ["k_miller_hex<MILLER_L0>", "k_miller_hex<MILLER_GROUPS>", "k_miller_hex<MILLER_GROUP_S>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_inv", "k_l0_fe", "k_l0_after",
                "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_gident_lines", "k_lines_fold<FOLD_GID>",
                "k_rlc_gident_miller", "k_rlc_gident_check", "k_rlc_chunk_lines", "k_lines_fold<FOLD_CHUNKS>",
                "k_rlc_check_chunks", "k_rlc_cident_lines", "k_lines_fold<FOLD_CID>", "k_rlc_cident_check",
@@ -396,6 +396,8 @@ def main():
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
+    ap.add_argument("--gident", type=int, default=0,
+                    help="level 1g (tbg_config.gident): 0 off, 1 unresolved groups to level 3, 2 to level 1.5")
     ap.add_argument("--inject", type=float, default=None,
                     help="fraction of partials replaced by invalid ones (side measurement; the headline is 0; "
                          "config5 defaults to 0.01)")
@@ -446,7 +448,7 @@ def main():
     # only the first `inflight` slots)
     e = eng.Engine(device, slots=max(args.inflight, 1) + (1 if args.api_batches else 0),
                    verify_mode=args.verify_mode, rlc_group=args.rlc_group,
-                   rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot)
+                   rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot, gident=args.gident)
     # `inflight` engine slots each hold `merge` independent caller batches
     # submitted together (tbg_submit_group: one device batch, one launch per
     # kernel for all of them) and stay resident; the timed region replays the
@@ -546,7 +548,7 @@ def main():
         "config": {"workload": WORKLOADS[args.workload].format(dvs=args.dvs, inject=args.inject),
                    "partials_per_step_per_gpu": int(len(b.identifiers)), "parallelism": f"shard{ws}",
                    "inflight_launches": args.inflight, "batches_per_launch": M,
-                   "rlc_group": group_used,
+                   "rlc_group": group_used, "gident": args.gident,
                    "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         "fallback_levels": fallback,

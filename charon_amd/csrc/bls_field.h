@@ -173,6 +173,16 @@ TBG_HD Fp fp_sub_l(const Fp& a, const Fp& b) {
   TBG_BOUND(fp_max_limb(r) < (1u << 31), "fp_sub_l limbs < 2^31");
   return r;
 }
+// Lazy 16p - a (a normalised): limbs < 2^29, unnormalised -- for a product
+// operand only (fp_mul_sum's column check covers it)
+TBG_HD Fp fp_neg_l(const Fp& a) {
+  TBG_BOUND(fp_ratio_p(a) <= 16.0, "fp_neg_l a <= 16p");
+  TBG_BOUND(fp_max_limb(a) < (1u << 28), "fp_neg_l a normalised");
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.l[i] = SUB16P_L[i] - a.l[i];
+  return r;
+}
 // normalise the limbs of a lazy value (same value)
 TBG_HD Fp fp_norm(const Fp& a) {
   Fp r = a;

@@ -13,9 +13,8 @@
 //
 // Layout: trio lane q = (lane & 15) % 3 as in bls_quad.h (5 trios per DPP
 // row, lane 15 idle); component c = (lane >> 4) & 1 (rows 0 and 2 hold c0,
-// rows 1 and 3 c1, partner = lane ^ 16, one ds_swizzle per word; see
-// TBG_HEX_SWIZZLE below for the permlane32 form).  Trio exchanges stay DPP row shifts on the
-// own component.  A wave carries 10 Fp12 values (60 of 64 lanes work).
+// rows 1 and 3 c1, partner = lane ^ 16, one ds_swizzle per word).  Trio
+// exchanges stay DPP row shifts on the own component.  A wave carries 10 Fp12 values (60 of 64 lanes work).
 //
 // Cross-component terms (the multiplications by xi = 1 + u hidden in the
 // Fp4 / Fp12 algebra) need the partner's component of ONE value per
@@ -177,36 +176,32 @@ TBG_HD bool hx_is_one_lane(uint32_t c, int q, const Fp4h& A) {
 #if defined(__HIP__)
 namespace tbg {
 
-// Where the component partner sits.  TBG_HEX_SWIZZLE = 1 (default): rows 0 / 1
-// (and 2 / 3) of the wave hold components 0 / 1 of the same five trios, the
-// partner is lane ^ 16, and the exchange is ONE ds_swizzle (the LDS crossbar
-// in xor mode, no LDS memory) per word.  0: halves of the wave, partner lane
-// ^ 32 by v_permlane32_swap -- which swaps between two registers, so every
-// word also took a copy and a per-half select (3 VALU instructions; 364
-// permlanes in k_miller_hex's loop body, profiles/r04).
-#ifndef TBG_HEX_SWIZZLE
-#define TBG_HEX_SWIZZLE 1
-#endif
+// Where the component partner sits: rows 0 / 1 (and 2 / 3) of the wave hold
+// components 0 / 1 of the same five trios, the partner is lane ^ 16, and the
+// exchange is ONE ds_swizzle (the LDS crossbar in xor mode, no LDS memory)
+// per word.  (Halves of the wave with v_permlane32_swap took a copy and a
+// per-half select besides -- 3 VALU instructions per word; measured slower,
+// round 4: profiles/r04/lazy/; removed.)
 // Fp12 slot of global thread t (UINT32_MAX for lane 15 of a row), and the
 // threads n slots need: 10 per wave.
 TBG_HD inline uint32_t hex_slot(uint32_t t) {
   const uint32_t l = t & 15u;
-  const uint32_t set = TBG_HEX_SWIZZLE ? (t >> 5) & 1u : (t >> 4) & 1u;  // which five trios
-  return l == 15u ? 0xFFFFFFFFu : (t >> 6) * 10u + set * 5u + l / 3u;
+  return l == 15u ? 0xFFFFFFFFu : (t >> 6) * 10u + ((t >> 5) & 1u) * 5u + l / 3u;
 }
 inline uint32_t hex_threads(uint32_t n) { return 64u * ((n + 9u) / 10u); }
-TBG_DEV uint32_t hex_c() { return TBG_HEX_SWIZZLE ? (threadIdx.x >> 4) & 1u : (threadIdx.x >> 5) & 1u; }
-
-// the partner lane's value
-TBG_DEV uint32_t hx_swap_u32(uint32_t v) {
-#if TBG_HEX_SWIZZLE
-  // bitmask mode within 32-lane groups: and 0x1f, or 0, xor 0x10 -> lane ^ 16
-  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
-#else
-  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return (threadIdx.x & 32u) ? r[0] : r[1];
+TBG_DEV uint32_t hex_c() { return (threadIdx.x >> 4) & 1u; }
+// lane (q, c) = (0, 0) of this thread's hexad: the one that takes list slots
+// and writes per-entry verdicts
+TBG_DEV bool hex_lead() { return quad_lane() == 0 && hex_c() == 0; }
+TBG_DEV uint32_t hex_lead_lane() { return (threadIdx.x - (uint32_t)quad_lane()) & ~16u; }
+// hexad kernels fit 256 VGPRs: two waves per SIMD
+#ifndef TBG_HEX_WAVES
+#define TBG_HEX_WAVES 2
 #endif
-}
+
+// the partner lane's value: ds_swizzle bitmask mode within 32-lane groups
+// (and 0x1f, or 0, xor 0x10 -> lane ^ 16)
+TBG_DEV uint32_t hx_swap_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F); }
 TBG_DEV Fp hx_swap(const Fp& x) {
   Fp r;
 #pragma unroll

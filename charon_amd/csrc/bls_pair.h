@@ -32,7 +32,7 @@ namespace tbg {
 
 // ---- per-lane pieces: par = lane parity, a / b own values, ap / bp partner's
 TBG_HD Fp pair_mul_lane(uint32_t par, const Fp& a, const Fp& ap, const Fp& b, const Fp& bp) {
-  const Fp nbp = fp_neg(bp);
+  const Fp nbp = fp_neg_l(bp);  // (lazy: a product operand only)
   return fp_mul2(a, fp_select(par != 0, bp, b), ap, fp_select(par != 0, b, nbp));
 }
 // (the lane's operands a, a' normalised: a' is subtracted; the two factors

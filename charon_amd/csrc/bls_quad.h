@@ -6,11 +6,11 @@
 //   A0 = (a_0, a_3) = (c0.c0, c1.c1)
 //   A1 = (a_1, a_4) = (c1.c0, c0.c2)
 //   A2 = (a_2, a_5) = (c0.c1, c1.c2)
-// Lane q = 0, 1, 2 of a lane group (the "quad": a trio of lanes of a DPP row
-// by default, see TBG_TRIO below) owns A_q.  A product is Karatsuba-3 over Fp4: every lane
+// Lane q = 0, 1, 2 of a lane group (the "quad": a trio of lanes of a DPP
+// row) owns A_q.  A product is Karatsuba-3 over Fp4: every lane
 // computes two Fp4 products (6 Fp2 products) instead of one lane computing
 // 18, and operands / partial products move between the lanes of the quad
-// with DPP quad_perm moves (full-rate VALU, no LDS).  The per-lane pieces
+// with DPP row shifts (full-rate VALU, no LDS).  The per-lane pieces
 // are plain functions so the host build can check the algebra by emulating
 // the quad (tests/hostcheck).
 #pragma once
@@ -129,14 +129,11 @@ namespace tbg {
 #define TBG_QUAD_FN __noinline__
 #endif
 
-// Lane groups.  TBG_TRIO = 1 (default): an Fp12 lives on a TRIO of
-// consecutive lanes of a 16-lane DPP row -- 5 trios per row, lane 15 idle,
-// so 60 of 64 lanes work; operands move with DPP row shifts (two per word
-// plus a select).  TBG_TRIO = 0: the quad layout (lanes 4k .. 4k + 3, lane 3
-// mirrors lane 2: 48 of 64 lanes work) with one quad_perm move per word.
-#ifndef TBG_TRIO
-#define TBG_TRIO 1
-#endif
+// Lane groups: an Fp12 lives on a TRIO of consecutive lanes of a 16-lane
+// DPP row -- 5 trios per row, lane 15 idle, so 60 of 64 lanes work; operands
+// move with DPP row shifts (two per word plus a select).  (The round-1 quad
+// layout -- lanes 4k .. 4k + 3 with lane 3 mirroring lane 2, one quad_perm
+// move per word -- kept 48 of 64 lanes busy and was slower; removed.)
 // exchange kinds: lane q of the group reads the value of lane ...
 enum QuadXch : int {
   QP_NEXT = 0,  // (q + 1) mod 3
@@ -155,7 +152,6 @@ TBG_DEV uint32_t dpp_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
 }
 
-#if TBG_TRIO
 // DPP row shifts: row_shl:n -- lane l reads lane l + n of its row; row_shr:n -- lane l - n.
 constexpr int DPP_SHL1 = 0x101, DPP_SHL2 = 0x102, DPP_SHR1 = 0x111, DPP_SHR2 = 0x112;
 TBG_DEV int quad_lane() { return (int)((threadIdx.x & 15u) % 3u); }
@@ -177,22 +173,6 @@ TBG_DEV uint32_t xch_u32(uint32_t v) {
   const uint32_t a = dpp_u32<DPP_SHL2>(v), b = dpp_u32<DPP_SHL1>(v);  // QP_B2
   return q == 0 ? a : (q == 1 ? b : v);
 }
-#else
-// quad_perm controls (lane q reads lane sel[q]); lane 3 behaves as lane 2.
-constexpr int QPERM[6] = {
-    1 | (2 << 2) | (0 << 4) | (0 << 6),  // NEXT
-    2 | (0 << 2) | (1 << 4) | (1 << 6),  // PREV
-    0 | (2 << 2) | (1 << 4) | (1 << 6),  // SW12
-    0x00, 0x55, 0xAA};                   // broadcast lane 0 / 1 / 2
-TBG_DEV int quad_lane() {
-  int q = (int)(threadIdx.x & 3);
-  return q > 2 ? 2 : q;
-}
-TBG_HD inline uint32_t fp12_slot(uint32_t t) { return t >> 2; }
-inline uint32_t fp12_threads(uint32_t n) { return 4u * n; }
-template <int K>
-TBG_DEV uint32_t xch_u32(uint32_t v) { return dpp_u32<QPERM[K]>(v); }
-#endif
 // lane 0 of this thread's group (the list-slot owner of push_ident)
 TBG_DEV uint32_t quad_lead_lane() { return threadIdx.x - (uint32_t)quad_lane(); }
 

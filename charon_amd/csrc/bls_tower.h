@@ -35,88 +35,14 @@ TBG_HD Fp2 fp2_mul_small(const Fp2& a, uint32_t k) { return {fp_mul_small(a.c0, 
 TBG_HD Fp2 fp2_add_l(const Fp2& a, const Fp2& b) { return {fp_add_l(a.c0, b.c0), fp_add_l(a.c1, b.c1)}; }
 TBG_HD Fp2 fp2_sub_l(const Fp2& a, const Fp2& b) { return {fp_sub_l(a.c0, b.c0), fp_sub_l(a.c1, b.c1)}; }
 
-// Fp2 product.  TBG_FP2_KARA=1: Karatsuba with lazy reduction —
-// the three half products a0*b0, a1*b1, (a0+a1)(b0+b1) are scanned column by
-// column and never reduced on their own; each column feeds two interleaved
-// Montgomery reductions:
-//   c0 = REDC(a0 b0 - a1 b1)          signed columns, arithmetic carries
-//   c1 = REDC((a0+a1)(b0+b1) - a0 b0 - a1 b1) = REDC(a0 b1 + a1 b0), whose
-//        columns are the non-negative a0_i b1_j + a1_i b0_j sums
-// Off by default: measured on MI355X it saves no time (isolated batch
-// 33.0 ms vs 32.4 ms with two fp_mul2) -- the extra 64-bit column
-// arithmetic and register pressure eat the 196 saved mul-adds.
-// 5 x 196 u32 mul-adds instead of 6 x 196 for two fp_mul2.  Column values
-// stay below 2^62.2 in magnitude (<= 14 products of < 2^58 for the sum
-// product, < 2^56 for the others, plus the m*p column and the carry).
-// c0 before the fix-up lies in (-a1 b1 / R, a0 b0 / R + p): with every
-// product < 2048 p^2 (= R p) that is (-p, 2p), and one conditional +p when
-// the top carry is negative brings it to [0, 2p).
-#ifndef TBG_FP2_KARA
-#define TBG_FP2_KARA 0
-#endif
-#if TBG_FP2_KARA
-TBG_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
-  TBG_BOUND(fp_ratio_p(a.c0) * fp_ratio_p(b.c0) < 2048.0 && fp_ratio_p(a.c1) * fp_ratio_p(b.c1) < 2048.0 &&
-                fp_ratio_p(a.c0) * fp_ratio_p(b.c1) + fp_ratio_p(a.c1) * fp_ratio_p(b.c0) < 2048.0,
-            "fp2_mul bound");
-  TBG_COUNT(196 * 5);
-  // limb-wise sums, NOT normalised (limbs < 2^29): the column identity
-  // sa_i sb_j - a0_i b0_j - a1_i b1_j = a0_i b1_j + a1_i b0_j needs it
-  Fp sa, sb;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    sa.l[i] = a.c0.l[i] + a.c1.l[i];
-    sb.l[i] = b.c0.l[i] + b.c1.l[i];
-  }
-  uint32_t m0[NL], m1[NL];
-  Fp r0, r1;
-  uint64_t acc0 = 0, acc1 = 0;  // acc0 holds a signed carry (two's complement)
-#pragma unroll
-  for (int k = 0; k < 2 * NL - 1; ++k) {
-    uint64_t p00[2] = {}, p11[2] = {}, pss[2] = {}, t0[2] = {}, t1[2] = {};
-    const int lo = k < NL ? 0 : k - NL + 1;
-    const int hi = k < NL ? k : NL - 1;
-#pragma unroll
-    for (int i = lo; i <= hi; ++i) {
-      p00[i & 1] += (uint64_t)a.c0.l[i] * b.c0.l[k - i];
-      p11[i & 1] += (uint64_t)a.c1.l[i] * b.c1.l[k - i];
-      pss[i & 1] += (uint64_t)sa.l[i] * sb.l[k - i];
-    }
-    const int mhi = k < NL ? k - 1 : NL - 1;
-#pragma unroll
-    for (int i = lo; i <= mhi; ++i) {
-      t0[i & 1] += (uint64_t)m0[i] * P_L[k - i];
-      t1[i & 1] += (uint64_t)m1[i] * P_L[k - i];
-    }
-    const uint64_t q00 = p00[0] + p00[1], q11 = p11[0] + p11[1];
-    uint64_t s0 = (q00 - q11) + ((t0[0] + t0[1]) + acc0);
-    uint64_t s1 = ((pss[0] + pss[1]) - (q00 + q11)) + ((t1[0] + t1[1]) + acc1);
-    if (k < NL) {
-      m0[k] = ((uint32_t)s0 * NINV) & LMASK;
-      m1[k] = ((uint32_t)s1 * NINV) & LMASK;
-      s0 += (uint64_t)m0[k] * P_L[0];
-      s1 += (uint64_t)m1[k] * P_L[0];
-    } else {
-      r0.l[k - NL] = (uint32_t)s0 & LMASK;
-      r1.l[k - NL] = (uint32_t)s1 & LMASK;
-    }
-    acc0 = (uint64_t)((int64_t)s0 >> 28);
-    acc1 = s1 >> 28;
-  }
-  r0.l[NL - 1] = (uint32_t)acc0;
-  r1.l[NL - 1] = (uint32_t)acc1;
-  const uint32_t neg = (uint32_t)((int64_t)acc0 >> 63);
-#pragma unroll
-  for (int i = 0; i < NL; ++i) r0.l[i] += P_L[i] & neg;
-  fp_normalize(r0);
-  return {r0, r1};
-}
-#else
+// Fp2 product: two REDC(a b + c d) (fp_mul2).  (A Karatsuba form with lazy
+// reduction -- 5 x 196 mul-adds instead of 6 x 196 -- measured no faster on
+// MI355X, round 1: the extra 64-bit column arithmetic and register pressure
+// eat the saved products; removed.)
 TBG_HD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   Fp nb1 = fp_neg(b.c1);
   return {fp_mul2(a.c0, b.c0, a.c1, nb1), fp_mul2(a.c0, b.c1, a.c1, b.c0)};
 }
-#endif
 
 TBG_HD Fp2 fp2_sqr(const Fp2& a) {
   Fp s = fp_add_l(a.c0, a.c1);

@@ -17,9 +17,6 @@
 
 namespace tbg {
 
-#ifndef TBG_HEX_WAVES
-#define TBG_HEX_WAVES 2
-#endif
 #ifndef TBG_HEX_HOIST
 #define TBG_HEX_HOIST 1
 #endif

@@ -21,8 +21,8 @@
 // duty, a bad duty to its bad partial; whatever the exponent tests cannot
 // pin down (two or more bad members) goes to level 3, the exact per-item
 // check -- so every partial's verdict is the one tbls.Verify would return.
-// One lane group (a "quad": a trio of lanes of a DPP row, bls_quad.h) runs
-// each product check over Miller lines
+// One lane group (a hexad: six lanes, bls_hex.h) runs each product check --
+// its Miller loop, final exponentiation and exponent test -- over Miller lines
 // stored in HBM: the H(m) lines are shared by all partials of a message, the
 // -g1 factor is folded into the lines of S / S_c / s_i.  Work lists of the
 // fallback levels are compacted on the device (atomic counters), so a clean
@@ -33,10 +33,11 @@
 #include "tbls_launch.h"
 #include "bls_h2c.h"
 #include "bls_lines.h"
-#include "bls_quad.h"
+#include "bls_hex.h"
 #include "bls_rlc.h"
 #include "bls_batchinv.h"
 #include "bls_wide.h"
+#include "bls_row.h"
 
 namespace tbg {
 
@@ -144,46 +145,9 @@ __global__ void TBG_LAUNCH k_rlc_group_lines(DevBatch B) {
   B.grp_state[g] = GRP_LINES;
 }
 
-// f *= line(H(m) lines at step idx) evaluated at affine P = (-x, y).  The
-// two evaluation products are split over the quad (lane 0: l1 (-x), lane 1:
-// l4 y) and broadcast, instead of every lane computing both.
-template <bool INL = false>
-__device__ __forceinline__ Fp4 quad_line_at(const Fp4& f, const uint32_t* lines, int idx, const Fp& nx, const Fp& y) {
-  const uint32_t* src = lines + LINE_WORDS * idx;
-  const bool first = quad_lane() == 0;
-  Fp2 l0, lk;
-  for (int i = 0; i < NL; ++i) {
-    l0.c0.l[i] = src[i];
-    l0.c1.l[i] = src[NL + i];
-    lk.c0.l[i] = first ? src[2 * NL + i] : src[4 * NL + i];
-    lk.c1.l[i] = first ? src[3 * NL + i] : src[5 * NL + i];
-  }
-  Fp2 e = fp2_mul_fp(lk, first ? nx : y);
-  return INL ? quad_line_in(f, l0, xch<QP_B0>(e), xch<QP_B1>(e)) : quad_line(f, l0, xch<QP_B0>(e), xch<QP_B1>(e));
-}
-template <bool INL = false>
-__device__ __forceinline__ Fp4 quad_line_folded(const Fp4& f, const uint32_t* lines, int idx) {
-  Line a = line_load(lines + LINE_WORDS * idx);
-  return INL ? quad_line_in(f, a.l0, a.l1, a.l4) : quad_line(f, a.l0, a.l1, a.l4);
-}
-
-// Quad-layout Fp12 in HBM: lane q < 3 owns one Fp4 (4 NL words).
+// Fp12 values in HBM in the quad layout: trio lane q's Fp4 at 4 NL words
+// per lane (hex_load / hex_store, bls_hex.h).
 constexpr int QUAD_WORDS = 4 * NL;
-__device__ __forceinline__ void quad_store(uint32_t* dst, const Fp4& A) {
-  int q = quad_lane();
-  if (TBG_TRIO == 0 && (threadIdx.x & 3) == 3) return;  // the quad layout's mirror lane
-  const Fp* f[4] = {&A.a.c0, &A.a.c1, &A.b.c0, &A.b.c1};
-  for (int k = 0; k < 4; ++k)
-    for (int j = 0; j < NL; ++j) dst[QUAD_WORDS * q + k * NL + j] = f[k]->l[j];
-}
-__device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
-  int q = quad_lane();
-  Fp4 A;
-  Fp* f[4] = {&A.a.c0, &A.a.c1, &A.b.c0, &A.b.c1};
-  for (int k = 0; k < 4; ++k)
-    for (int j = 0; j < NL; ++j) f[k]->l[j] = src[QUAD_WORDS * q + k * NL + j];
-  return A;
-}
 
 // Level 1, Miller part: one hexad per (group, chunk of rlc_chunk duties),
 // plus one per group for the group's S pair alone (k_miller_hex.hip).
@@ -192,16 +156,16 @@ __device__ __forceinline__ Fp4 quad_load(const uint32_t* src) {
 // apart from S, a failed group can re-check its chunks (level 1.5) from these
 // same products with only S_c's Miller loop added.
 
-// Level 1, final part: one quad per group multiplies its chunks' products
+// Level 1, final part: one hexad per group multiplies its chunks' products
 // (the S chunk included) and runs the one final exponentiation of the group.
-__global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_group_final(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t G = B.rlc_group, C = B.rlc_chunk;
   uint32_t n_groups = (B.n_duties + G - 1) / G;
   uint32_t nq = (G + C - 1) / C + 1;
-  uint32_t g = fp12_slot(t);
+  uint32_t g = hex_slot(t);
   if (g >= n_groups) return;
-  const bool lead = quad_lane() == 0;
+  const bool lead = hex_lead();
   if (B.grp_state[g] != GRP_LINES) return;  // empty groups have nothing to resolve; GRP_FAIL stays failed
   uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
   for (uint32_t d = d0; d < d1; ++d) {
@@ -211,20 +175,20 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
     }
   }
   const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nq * g;
-  Fp4 f = quad_load(base);
-  for (uint32_t c = 1; c < nq; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
-  f = quad_final_exp_in(quad_conj(f));
-  bool ok = quad_is_one(f);
+  Fp4h f = hex_load(base);
+  for (uint32_t c = 1; c < nq; ++c) f = hex_mul_ni(f, hex_load(base + (size_t)3 * QUAD_WORDS * c));
+  f = hex_final_exp_in(hex_conj(f));
+  bool ok = hex_is_one(f);
   if (!ok && B.gident) {
-    // level 1g: the group's value A_g, and the group in the list (quad-uniform)
+    // level 1g: the group's value A_g, and the group in the list (hexad-uniform)
     uint32_t m = 0;
     for (uint32_t d = d0; d < d1; ++d)
       if (rlc_combinable(B, d)) m += rlc_candidates(B, d);
     if (m >= 2) {
       uint32_t slot = 0;
       if (lead) slot = atomicAdd(&B.counters[CNT_GID], 1u);
-      slot = (uint32_t)__shfl((int)slot, (int)quad_lead_lane());
-      quad_store(B.grp_fe + (size_t)3 * QUAD_WORDS * slot, f);
+      slot = (uint32_t)__shfl((int)slot, (int)hex_lead_lane());
+      hex_store(B.grp_fe + (size_t)3 * QUAD_WORDS * slot, f);
       if (lead) {
         B.gid_list[slot] = g;
         B.grp_state[g] = GRP_GID;
@@ -236,44 +200,137 @@ __global__ void TBG_LAUNCH k_rlc_group_final(DevBatch B) {
 }
 
 // ------------------------------------------------------------------ level 0
-// One quad per group: the product of its P-chunk values (k_rlc_miller_chunks,
+// One hexad per group: the product of its P-chunk values (k_miller_hex,
 // MILLER_L0); a combined duty whose H(m) is unusable makes level 0 fail.
-__global__ void TBG_LAUNCH_N(2) k_l0_fold(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_l0_fold(DevBatch B) {
   TBG_URGENT();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk;
   const uint32_t n_groups = (B.n_duties + G - 1) / G, nch = (G + C - 1) / C, nq = nch + 1;
-  const uint32_t g = fp12_slot(t);
+  const uint32_t g = hex_slot(t);
   if (g >= n_groups || B.counters[CNT_L0_BAD]) return;
   const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
   for (uint32_t d = d0; d < d1; ++d) {
     if (B.dv_state[d] == RLC_COMBINED && B.h_status[B.duty_msg[d]] != 0) {
-      if (quad_lane() == 0) B.counters[CNT_L0_BAD] = 1;
+      if (hex_lead()) B.counters[CNT_L0_BAD] = 1;
       return;
     }
   }
   const uint32_t* base = B.chunk_f + (size_t)3 * QUAD_WORDS * nq * g;
-  Fp4 f = quad_load(base);
-  for (uint32_t c = 1; c < nch; ++c) f = quad_mul_in(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
-  quad_store(B.grp_f + (size_t)3 * QUAD_WORDS * g, f);
+  Fp4h f = hex_load(base);
+  for (uint32_t c = 1; c < nch; ++c) f = hex_mul(f, hex_load(base + (size_t)3 * QUAD_WORDS * c));
+  hex_store(B.grp_f + (size_t)3 * QUAD_WORDS * g, f);
 }
 
-// Product tree, one quad per L0_TREE_FAN values of grp_f[in .. in + n).
-__global__ void TBG_LAUNCH_N(2) k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32_t out) {
+// Product tree, one hexad per L0_TREE_FAN values of grp_f[in .. in + n).
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_l0_tree(DevBatch B, uint32_t in, uint32_t n, uint32_t out) {
   TBG_URGENT();
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t q = fp12_slot(t), a0 = q * L0_TREE_FAN;
-  if (a0 >= n || B.counters[CNT_L0_BAD]) return;
-  const uint32_t a1 = min(a0 + L0_TREE_FAN, n);
-  Fp4 f = quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a0));
-  for (uint32_t a = a0 + 1; a < a1; ++a) f = quad_mul_in(f, quad_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
-  quad_store(B.grp_f + (size_t)3 * QUAD_WORDS * (out + q), f);
+  const uint32_t q = hex_slot(t);
+  if (q == 0xFFFFFFFFu || q * L0_TREE_FAN >= n || B.counters[CNT_L0_BAD]) return;
+  const uint32_t a0 = q * L0_TREE_FAN, a1 = min(a0 + L0_TREE_FAN, n);
+  Fp4h f = hex_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a0));
+  for (uint32_t a = a0 + 1; a < a1; ++a) f = hex_mul(f, hex_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
+  hex_store(B.grp_f + (size_t)3 * QUAD_WORDS * (out + q), f);
 }
 
-// ONE wave: the last <= L0_TREE_FAN values times the S pair's product, one
-// final exponentiation for the whole batch -- the latency tail of every
-// level-0 launch, so the value is spread over the wave's lanes (bls_wide.h:
-// one Fp product per lane per step) instead of one trio.
+// The last <= L0_TREE_FAN values times the S pair's product, one final
+// exponentiation for the whole batch -- the latency tail of every level-0
+// launch.  TBG_L0_FINAL selects its layout:
+//   2 (default) on ROWS (bls_row.h: one Fp per 16-lane row, each Montgomery
+//     product limb-parallel over its row): k_l0_final forms f, k_l0_inv
+//     inverts it on one lane (the tower inverse; its out-of-line calls would
+//     pin the row kernel's 576 threads to their register budget), k_l0_fe
+//     exponentiates;
+//   1 on ONE hexad (bls_hex.h);
+//   0 over the lanes of one wave (bls_wide.h: one Fp product per lane).
+#ifndef TBG_L0_FINAL
+#define TBG_L0_FINAL 2
+#endif
+#if TBG_L0_FINAL == 2
+constexpr uint32_t L0_FINAL_THREADS = 16 * 36;  // 36 rows: a product step's Fp products
+struct RowDevExec {
+  template <class Fn>
+  __device__ void operator()(Fn&& fn) {
+    fn((int)(threadIdx.x >> 4));
+    __syncthreads();
+  }
+};
+// f and f^-1 between the three kernels: two spare grp_f entries (12 x 14
+// signed limbs each, the row words; grp_f_entries keeps 40 spare)
+__device__ __forceinline__ int32_t* l0_f_spare(const DevBatch& B, int k) {
+  const uint32_t n_groups = (B.n_duties + B.rlc_group - 1) / B.rlc_group;
+  return (int32_t*)(B.grp_f + (size_t)3 * QUAD_WORDS * (grp_f_entries(n_groups) - 1 - k));
+}
+__global__ void __launch_bounds__(L0_FINAL_THREADS) k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
+  TBG_URGENT();
+  if (B.counters[CNT_L0_BAD]) return;  // (workgroup-uniform)
+  __shared__ RowSlots S;
+  RowDevExec ex;
+  const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
+  auto load = [&](int slot, const uint32_t* src) {
+    if (r < RW_FP) row_st(S.v[slot][r], row_from_limbs(src + r * NL));
+  };
+  ex([&](int) { load(0, B.batch_f); });
+  for (uint32_t a = 0; a < n; ++a) {
+    ex([&](int) { load(1, B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)); });
+    row_mul_to(ex, S, 0, 0, 1);
+  }
+  if (r < RW_FP && j < NL) l0_f_spare(B, 0)[r * NL + j] = S.v[0][r][j];
+}
+__global__ void __launch_bounds__(64) k_l0_inv(DevBatch B) {
+  TBG_URGENT();
+  if (B.counters[CNT_L0_BAD] || threadIdx.x != 0) return;
+  const int32_t* f = l0_f_spare(B, 0);
+  Fp4 A[3];
+  for (int q = 0; q < 3; ++q) {
+    A[q].a.c0 = fp_from_signed(f + (4 * q) * NL);
+    A[q].a.c1 = fp_from_signed(f + (4 * q + 1) * NL);
+    A[q].b.c0 = fp_from_signed(f + (4 * q + 2) * NL);
+    A[q].b.c1 = fp_from_signed(f + (4 * q + 3) * NL);
+  }
+  const Fp12 v = fp12_inv(quad_to_fp12(A[0], A[1], A[2]));
+  int32_t* out = l0_f_spare(B, 1);
+  for (int q = 0; q < 3; ++q) {
+    const Fp4 c = quad_from_fp12(q, v);
+    const Fp* w[4] = {&c.a.c0, &c.a.c1, &c.b.c0, &c.b.c1};
+    for (int k = 0; k < 4; ++k)
+      for (int i = 0; i < NL; ++i) out[(4 * q + k) * NL + i] = (int32_t)w[k]->l[i];
+  }
+}
+__global__ void __launch_bounds__(L0_FINAL_THREADS) k_l0_fe(DevBatch B) {
+  TBG_URGENT();
+  if (B.counters[CNT_L0_BAD]) return;
+  __shared__ RowSlots S;
+  RowDevExec ex;
+  const int r = threadIdx.x >> 4;
+  ex([&](int) {
+    if (r < RW_FP) {
+      row_st(S.v[0][r], row_from_limbs((const uint32_t*)l0_f_spare(B, 0) + r * NL));
+      row_st(S.v[5][r], row_from_limbs((const uint32_t*)l0_f_spare(B, 1) + r * NL));
+    }
+  });
+  row_final_exp_inv(ex, S);
+  if (threadIdx.x == 0 && row_is_one(S.v[0])) B.counters[CNT_L0_OK] = 1;
+}
+static void launch_l0_final(const DevBatch& B, uint32_t in, uint32_t n, hipStream_t st) {
+  TBG_KLAUNCH(k_l0_final, dim3(1), dim3(L0_FINAL_THREADS), st, B, in, n);
+  TBG_KLAUNCH(k_l0_inv, dim3(1), dim3(64), st, B);
+  TBG_KLAUNCH(k_l0_fe, dim3(1), dim3(L0_FINAL_THREADS), st, B);
+}
+#elif TBG_L0_FINAL == 1
+__global__ void __launch_bounds__(64) k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
+  TBG_URGENT();
+  if (B.counters[CNT_L0_BAD] || hex_slot(threadIdx.x) != 0) return;  // (one hexad: lanes 0..2, 16..18)
+  Fp4h f = hex_load(B.batch_f);
+  for (uint32_t a = 0; a < n; ++a) f = hex_mul_ni(f, hex_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
+  f = hex_final_exp_in(f);
+  if (hex_is_one(f) && hex_lead()) B.counters[CNT_L0_OK] = 1;
+}
+static void launch_l0_final(const DevBatch& B, uint32_t in, uint32_t n, hipStream_t st) {
+  TBG_KLAUNCH(k_l0_final, dim3(1), dim3(64), st, B, in, n);
+}
+#else
 struct WideDevExec {
   template <class Fn>
   __device__ void operator()(Fn&& fn) {
@@ -300,6 +357,10 @@ __global__ void __launch_bounds__(64) k_l0_final(DevBatch B, uint32_t in, uint32
   wide_final_exp(ex, S);
   if (l == 0 && wide_is_one(S.v[0])) B.counters[CNT_L0_OK] = 1;
 }
+static void launch_l0_final(const DevBatch& B, uint32_t in, uint32_t n, hipStream_t st) {
+  TBG_KLAUNCH(k_l0_final, dim3(1), dim3(64), st, B, in, n);
+}
+#endif
 
 // One thread per group: after a level-0 pass every group with a combined
 // duty is accepted (k_rlc_resolve_groups marks its candidates valid).
@@ -367,19 +428,34 @@ __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
 }
 
 
-// The fallback checks run their Miller loops and final exponentiations with
-// the squarings / line products inline (no scratch-stack call per step), as
-// the level-1 kernels do; TBG_FALLBACK_INL=0 builds the out-of-line form (A/B).
-#ifndef TBG_FALLBACK_INL
-#define TBG_FALLBACK_INL 1
-#endif
-#if TBG_FALLBACK_INL
-#define FB_SQR quad_sqr_in
-#define FB_FE quad_final_exp_in
-#else
-#define FB_SQR quad_sqr
-#define FB_FE quad_final_exp
-#endif
+// The fallback checks' Miller loops: f *= the step's folded lines (S-side,
+// -g1 folded in) and the H(m) lines at each listed point; squarings and line
+// products inline in the kernel loop (no scratch-stack call per step).
+template <class F>
+__device__ __forceinline__ Fp4h hex_miller(F&& step) {
+  Fp4h f = hex_one();
+  int idx = 0;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    if (b != 62) f = hex_sqr(f);
+    const int steps = ((X_ABS >> b) & 1) ? 2 : 1;
+#pragma unroll 1
+    for (int s = 0; s < steps; ++s, ++idx) f = step(f, idx);
+  }
+  return f;
+}
+
+// The exponent test's search: the w in 1..n with A^w == A' (inv_a2 = A'^-1),
+// 0 if none (hexad-uniform: hex_is_one agrees on all six lanes).
+__device__ __forceinline__ uint32_t hex_find_power(const Fp4h& A, const Fp4h& inv_a2, uint32_t n) {
+  Fp4h Aw = A;
+#pragma unroll 1
+  for (uint32_t w = 1; w <= n; ++w) {
+    if (hex_is_one(hex_mul_ni(Aw, inv_a2))) return w;
+    Aw = hex_mul_ni(Aw, A);
+  }
+  return 0;
+}
 
 // ---------------------------------------------------------- identification
 // The exponent test (Lee, Cheon and Hong, "Finding invalid signatures in
@@ -398,32 +474,32 @@ __global__ void TBG_LAUNCH k_rlc_chunk_lines(DevBatch B) {
 // (the only bad member's product IS the chunk's).
 
 // A failed duty with several candidates goes to level 2b with its A (every
-// lane of the quad stores its part; the lead takes the list slot).
-__device__ __forceinline__ void push_ident(const DevBatch& B, uint32_t d, const Fp4& A, bool lead) {
+// lane of the hexad stores its part; the lead takes the list slot).
+__device__ __forceinline__ void push_ident(const DevBatch& B, uint32_t d, const Fp4h& A, bool lead) {
   uint32_t slot = 0;
   if (lead) {
     slot = atomicAdd(&B.counters[CNT_DUTIES], 1u);
     B.id_list[slot] = d;
   }
-  slot = (uint32_t)__shfl((int)slot, (int)quad_lead_lane());
-  quad_store(B.id_fe + (size_t)3 * QUAD_WORDS * slot, A);
+  slot = (uint32_t)__shfl((int)slot, (int)hex_lead_lane());
+  hex_store(B.id_fe + (size_t)3 * QUAD_WORDS * slot, A);
 }
 // A duty known to be bad: one candidate -> that partial is invalid (the check
 // was its own, scaled by r != 0); several -> level 2b.
-__device__ __forceinline__ void resolve_bad_duty(const DevBatch& B, uint32_t d, const Fp4& A, bool lead) {
+__device__ __forceinline__ void resolve_bad_duty(const DevBatch& B, uint32_t d, const Fp4h& A, bool lead) {
   if (rlc_candidates(B, d) > 1) push_ident(B, d, A, lead);
   else if (lead) rlc_mark(B, d, TBG_PS_INVALID);
 }
 
-// Level 1.5 check: one quad per listed chunk: its stored P-pair product
+// Level 1.5 check: one hexad per listed chunk: its stored P-pair product
 // times the Miller loop of S_c, one final exponentiation.  Pass -> the
 // chunk's duties are valid; fail -> a lone duty is resolved at once, several
 // go to level 1.5b with the chunk's value (a degenerate S_c: level 3).
-__global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_check_chunks(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = fp12_slot(t) + B.fb_base;  // (fp12_slot's idle-lane value stays out of range)
-  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_CHUNKS] || !fb_in_pass(B, k)) return;
-  const bool lead = quad_lane() == 0;
+  uint32_t k = hex_slot(t) + B.fb_base;
+  if (hex_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_CHUNKS] || !fb_in_pass(B, k)) return;
+  const bool lead = hex_lead();
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C, nq = nch + 1;
   const uint32_t entry = B.chunk_list[k], qc = entry & ~CHUNK_DEGENERATE, g = qc / nch, c = qc % nch;
   const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
@@ -434,16 +510,10 @@ __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
     return;
   }
   const uint32_t* ls = B.chunk_lines + fb_slot(B, k);
-  Fp4 f = quad_one();
-  int idx = 0;
-  for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = FB_SQR(f);
-    int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-    for (int s = 0; s < steps; ++s, ++idx) f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
-  }
-  f = quad_mul(f, quad_load(B.chunk_f + (size_t)3 * QUAD_WORDS * (g * nq + c)));
-  f = FB_FE(quad_conj(f));
-  if (quad_is_one(f)) {
+  Fp4h f = hex_miller([&](const Fp4h& x, int idx) { return hex_line_folded(x, ls, idx); });
+  f = hex_mul_ni(f, hex_load(B.chunk_f + (size_t)3 * QUAD_WORDS * (g * nq + c)));
+  f = hex_final_exp_in(hex_conj(f));
+  if (hex_is_one(f)) {
     if (lead)
       for (uint32_t d = d0; d < d1; ++d)
         if (rlc_combinable(B, d)) rlc_mark(B, d, TBG_PS_VALID);
@@ -456,7 +526,7 @@ __global__ void TBG_LAUNCH k_rlc_check_chunks(DevBatch B) {
     resolve_bad_duty(B, lone, f, lead);
     return;
   }
-  quad_store(B.chunk_fe + (size_t)3 * QUAD_WORDS * k, f);
+  hex_store(B.chunk_fe + (size_t)3 * QUAD_WORDS * k, f);
   if (lead) B.cid_list[atomicAdd(&B.counters[CNT_CID], 1u)] = k;
 }
 
@@ -491,49 +561,38 @@ __global__ void TBG_LAUNCH k_rlc_cident_lines(DevBatch B) {
   B.pend_pts[j] = Sa;  // lines: k_lines_fold<FOLD_CID>
 }
 
-// Level 1.5b check: one quad per entry computes A'_c over the chunk's duties
+// Level 1.5b check: one hexad per entry computes A'_c over the chunk's duties
 // and tests A_c^w == A'_c.  Found -> the other duties are valid and duty w
 // is resolved with A = A_c; not found (two or more bad duties, rare) -> the
 // chunk's candidates go to level 3.
-__global__ void TBG_LAUNCH k_rlc_cident_check(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_cident_check(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t j = fp12_slot(t) + B.fb_base;
-  if (fp12_slot(t) == 0xFFFFFFFFu || j >= B.counters[CNT_CID] || !fb_in_pass(B, j)) return;
-  const bool lead = quad_lane() == 0;
+  uint32_t j = hex_slot(t) + B.fb_base;
+  if (hex_slot(t) == 0xFFFFFFFFu || j >= B.counters[CNT_CID] || !fb_in_pass(B, j)) return;
+  const bool lead = hex_lead();
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C;
   const uint32_t entry = B.cid_list[j], k = entry & ~ID_DEGENERATE;
   const uint32_t qc = B.chunk_list[k], g = qc / nch, c = qc % nch;
   const uint32_t d0 = g * G + c * C, d1 = min(min(d0 + C, g * G + G), B.n_duties);
   uint32_t found = 0, n = 0;
   for (uint32_t d = d0; d < d1; ++d) n += rlc_combinable(B, d) ? 1u : 0u;
-  const Fp4 A = quad_load(B.chunk_fe + (size_t)3 * QUAD_WORDS * k);
+  const Fp4h A = hex_load(B.chunk_fe + (size_t)3 * QUAD_WORDS * k);
   if (!(entry & ID_DEGENERATE)) {
     const uint32_t* ls = B.cid_lines + fb_slot(B, j);
-    const G1A* wp = B.cid_p + (size_t)C * j;
-    Fp4 f = quad_one();
-    int idx = 0;
-    for (int b = 62; b >= 0; --b) {
-      if (b != 62) f = FB_SQR(f);
-      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-      for (int s = 0; s < steps; ++s, ++idx) {
-        f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
-        uint32_t r = 0;
-        for (uint32_t d = d0; d < d1; ++d) {
-          if (!rlc_combinable(B, d)) continue;
-          const G1A& P = wp[r++];
-          f = quad_line_at<TBG_FALLBACK_INL>(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
-        }
+    const G1A* wp = B.cid_p + (size_t)C * j;  // (-x, y)
+    const Fp4h f = hex_miller([&](Fp4h x, int idx) {
+      x = hex_line_folded(x, ls, idx);
+      uint32_t r = 0;
+#pragma unroll 1
+      for (uint32_t d = d0; d < d1; ++d) {
+        if (!rlc_combinable(B, d)) continue;
+        const G1A& P = wp[r++];
+        x = hex_line_at(x, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
       }
-    }
-    const Fp4 inv_a2 = FB_FE(f);  // (A'_c)^-1: the conjugate is the inverse in GT
-    Fp4 Aw = A;
-    for (uint32_t w = 1; w <= n; ++w) {  // quad-uniform: quad_is_one agrees on all lanes
-      if (quad_is_one(quad_mul(Aw, inv_a2))) {
-        found = w;
-        break;
-      }
-      Aw = quad_mul(Aw, A);
-    }
+      return x;
+    });
+    // (A'_c)^-1: the conjugate is the inverse in GT
+    found = hex_find_power(A, hex_final_exp_in(f), n);
   }
   uint32_t w = 0, bad = d0;
   for (uint32_t d = d0; d < d1; ++d) {
@@ -573,13 +632,13 @@ __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
   B.pend_pts[k] = Sa;  // lines: k_lines_fold<FOLD_IDENT>
 }
 
-// Level 2b check: one quad per entry computes A'_d and tests A_d^w == A'_d.
+// Level 2b check: one hexad per entry computes A'_d and tests A_d^w == A'_d.
 // Found -> partial w invalid, the others valid; not found -> level 3.
-__global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_ident_check(DevBatch B) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = fp12_slot(t) + B.fb_base;
-  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k)) return;
-  const bool lead = quad_lane() == 0;
+  uint32_t k = hex_slot(t) + B.fb_base;
+  if (hex_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k)) return;
+  const bool lead = hex_lead();
   const uint32_t entry = B.id_list[k], d = entry & ~ID_DEGENERATE;
   uint32_t found = 0;
   if (!(entry & ID_DEGENERATE)) {
@@ -587,27 +646,9 @@ __global__ void TBG_LAUNCH k_rlc_ident_check(DevBatch B) {
     Fp nx = fp_reduce(fp_neg(P.x));
     const uint32_t* ls = B.id_lines + fb_slot(B, k);
     const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d];
-    Fp4 f = quad_one();
-    int idx = 0;
-    for (int b = 62; b >= 0; --b) {
-      if (b != 62) f = FB_SQR(f);
-      int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-      for (int s = 0; s < steps; ++s, ++idx) {
-        f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
-        f = quad_line_at<TBG_FALLBACK_INL>(f, lh, idx, nx, P.y);
-      }
-    }
-    const Fp4 inv_a2 = FB_FE(f);
-    const Fp4 A = quad_load(B.id_fe + (size_t)3 * QUAD_WORDS * k);
-    const uint32_t n = rlc_candidates(B, d);
-    Fp4 Aw = A;
-    for (uint32_t w = 1; w <= n; ++w) {
-      if (quad_is_one(quad_mul(Aw, inv_a2))) {
-        found = w;
-        break;
-      }
-      Aw = quad_mul(Aw, A);
-    }
+    const Fp4h f = hex_miller([&](Fp4h x, int idx) { return hex_line_at(hex_line_folded(x, ls, idx), lh, idx, nx, P.y); });
+    const Fp4h inv_a2 = hex_final_exp_in(f);
+    found = hex_find_power(hex_load(B.id_fe + (size_t)3 * QUAD_WORDS * k), inv_a2, rlc_candidates(B, d));
   }
   if (!lead) return;
   if (!found) {
@@ -708,13 +749,13 @@ __device__ __forceinline__ void push_group_chunks(const DevBatch& B, uint32_t g)
   }
 }
 
-// Level 1g Miller part, as level 1's: one quad per (entry, chunk of
-// rlc_chunk duties) over the duties' (P'_d, H(m_d)) pairs, and one quad per
+// Level 1g Miller part, as level 1's: one hexad per (entry, chunk of
+// rlc_chunk duties) over the duties' (P'_d, H(m_d)) pairs, and one hexad per
 // entry for the S' pair (its folded lines), each product into gid_f.
-__global__ void TBG_LAUNCH k_rlc_gident_miller(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_gident_miller(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nch = (G + C - 1) / C, nq = nch + 1;
-  const uint32_t s = fp12_slot(t);
+  const uint32_t s = hex_slot(t);
   if (s == 0xFFFFFFFFu) return;
   const uint32_t k = s / nq + B.fb_base, c = s % nq;
   if (k >= B.counters[CNT_GID] || !fb_in_pass(B, k)) return;
@@ -723,22 +764,18 @@ __global__ void TBG_LAUNCH k_rlc_gident_miller(DevBatch B) {
   const uint32_t g = entry, gd0 = g * G, gd1 = min(gd0 + G, B.n_duties);
   const uint32_t d0 = c == nch ? gd0 : min(gd0 + c * C, gd1), d1 = c == nch ? gd0 : min(d0 + C, gd1);
   const uint32_t* ls = B.gid_lines + fb_slot(B, k);
-  const G1A* wp = B.gid_p + (size_t)G * k;
-  Fp4 f = quad_one();
-  int idx = 0;
-  for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = FB_SQR(f);
-    int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-    for (int st = 0; st < steps; ++st, ++idx) {
-      if (c == nch) f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
-      for (uint32_t d = d0; d < d1; ++d) {
-        if (!rlc_combinable(B, d)) continue;
-        const G1A& P = wp[d - gd0];
-        f = quad_line_at<TBG_FALLBACK_INL>(f, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
-      }
+  const G1A* wp = B.gid_p + (size_t)G * k;  // (-x, y)
+  const Fp4h f = hex_miller([&](Fp4h x, int idx) {
+    if (c == nch) x = hex_line_folded(x, ls, idx);
+#pragma unroll 1
+    for (uint32_t d = d0; d < d1; ++d) {
+      if (!rlc_combinable(B, d)) continue;
+      const G1A& P = wp[d - gd0];
+      x = hex_line_at(x, B.h_lines + (size_t)LINES_WORDS * B.duty_msg[d], idx, P.x, P.y);
     }
-  }
-  quad_store(B.gid_f + (size_t)3 * QUAD_WORDS * ((size_t)k * nq + c), f);
+    return x;
+  });
+  hex_store(B.gid_f + (size_t)3 * QUAD_WORDS * ((size_t)k * nq + c), f);
 }
 
 // Candidates of an unresolved level-1g group up to which they all go to
@@ -747,18 +784,18 @@ __global__ void TBG_LAUNCH k_rlc_gident_miller(DevBatch B) {
 #define TBG_GID_L3_MAX 40u
 #endif
 
-// Level 1g check: one quad per entry multiplies its products into A'_g and
+// Level 1g check: one hexad per entry multiplies its products into A'_g and
 // tests A_g^w == A'_g.  Found -> candidate w invalid, the group's other
 // candidates valid; not found (two or more bad partials) or degenerate ->
 // the group's candidates go to the exact per-partial level (the levels
 // between cost a final exponentiation of latency each whatever their list
 // length, profiles/r03/gident/) -- or, with TBG_GIDENT=2, its chunks to
 // level 1.5 as the round-2 order had them.
-__global__ void TBG_LAUNCH k_rlc_gident_check(DevBatch B) {
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_gident_check(DevBatch B) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t k = fp12_slot(t) + B.fb_base;
-  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_GID] || !fb_in_pass(B, k)) return;
-  const bool lead = quad_lane() == 0;
+  const uint32_t k = hex_slot(t) + B.fb_base;
+  if (hex_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_GID] || !fb_in_pass(B, k)) return;
+  const bool lead = hex_lead();
   const uint32_t G = B.rlc_group, C = B.rlc_chunk, nq = (G + C - 1) / C + 1;
   const uint32_t entry = B.gid_list[k], g = entry & ~ID_DEGENERATE;
   const uint32_t d0 = g * G, d1 = min(d0 + G, B.n_duties);
@@ -767,18 +804,10 @@ __global__ void TBG_LAUNCH k_rlc_gident_check(DevBatch B) {
     if (rlc_combinable(B, d)) m += rlc_candidates(B, d);
   if (!(entry & ID_DEGENERATE)) {
     const uint32_t* base = B.gid_f + (size_t)3 * QUAD_WORDS * ((size_t)k * nq);
-    Fp4 f = quad_load(base);
-    for (uint32_t c = 1; c < nq; ++c) f = quad_mul(f, quad_load(base + (size_t)3 * QUAD_WORDS * c));
-    const Fp4 inv_a2 = FB_FE(f);  // (A'_g)^-1
-    const Fp4 A = quad_load(B.grp_fe + (size_t)3 * QUAD_WORDS * k);
-    Fp4 Aw = A;
-    for (uint32_t w = 1; w <= m; ++w) {  // quad-uniform
-      if (quad_is_one(quad_mul(Aw, inv_a2))) {
-        found = w;
-        break;
-      }
-      Aw = quad_mul(Aw, A);
-    }
+    Fp4h f = hex_load(base);
+    for (uint32_t c = 1; c < nq; ++c) f = hex_mul_ni(f, hex_load(base + (size_t)3 * QUAD_WORDS * c));
+    const Fp4h inv_a2 = hex_final_exp_in(f);  // (A'_g)^-1
+    found = hex_find_power(hex_load(B.grp_fe + (size_t)3 * QUAD_WORDS * k), inv_a2, m);
   }
   if (!lead) return;
   if (!found) {
@@ -824,12 +853,12 @@ __global__ void TBG_LAUNCH k_lines_sig_list(DevBatch B) {
   g2_lines_t<true>(B.sig_aff[i], nx, fp_from_const(G1_NEG_Y), B.sig_lines + fb_slot(B, k));
 }
 
-// Level 3 check: one quad per listed partial, the exact CoreVerify.
-__global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
+// Level 3 check: one hexad per listed partial, the exact CoreVerify.
+__global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_verify_list(DevBatch B, const G1A* pk_aff) {
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = fp12_slot(t) + B.fb_base;
-  if (fp12_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_PARTIALS] || !fb_in_pass(B, k)) return;
-  const bool lead = quad_lane() == 0;
+  uint32_t k = hex_slot(t) + B.fb_base;
+  if (hex_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_PARTIALS] || !fb_in_pass(B, k)) return;
+  const bool lead = hex_lead();
   uint32_t i = B.part_list[k];
   uint32_t m = B.duty_msg[B.partial_duty[i]];
   if (B.h_status[m] != 0) {
@@ -840,18 +869,9 @@ __global__ void TBG_LAUNCH k_verify_list(DevBatch B, const G1A* pk_aff) {
   Fp nx = fp_reduce(fp_neg(pk.x));
   const uint32_t* ls = B.sig_lines + fb_slot(B, k);
   const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * m;
-  Fp4 f = quad_one();
-  int idx = 0;
-  for (int b = 62; b >= 0; --b) {
-    if (b != 62) f = FB_SQR(f);
-    int steps = ((X_ABS >> b) & 1) ? 2 : 1;
-    for (int s = 0; s < steps; ++s, ++idx) {
-      f = quad_line_folded<TBG_FALLBACK_INL>(f, ls, idx);
-      f = quad_line_at<TBG_FALLBACK_INL>(f, lh, idx, nx, pk.y);
-    }
-  }
-  f = FB_FE(quad_conj(f));
-  bool ok = quad_is_one(f);
+  Fp4h f = hex_miller([&](Fp4h x, int idx) { return hex_line_at(hex_line_folded(x, ls, idx), lh, idx, nx, pk.y); });
+  f = hex_final_exp_in(hex_conj(f));
+  const bool ok = hex_is_one(f);
   if (lead) B.partial_status[i] = ok ? TBG_PS_VALID : TBG_PS_INVALID;
 }
 
@@ -903,16 +923,16 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     if (B.rlc_batch) {
       // level 0: the P chunks (kept for the group levels) and S, one product
       launch_l0_miller_hex(B, st);
-      TBG_KLAUNCH(k_l0_fold, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
+      TBG_KLAUNCH(k_l0_fold, grid_for(hex_threads(n_groups)), dim3(kBlock), st, B);
       uint32_t in = 0, n = n_groups, out = n_groups;
       while (n > L0_TREE_FAN) {
         const uint32_t m = (n + L0_TREE_FAN - 1) / L0_TREE_FAN;
-        TBG_KLAUNCH(k_l0_tree, grid_for(fp12_threads(m)), dim3(kBlock), st, B, in, n, out);
+        TBG_KLAUNCH(k_l0_tree, grid_for(hex_threads(m)), dim3(kBlock), st, B, in, n, out);
         in = out;
         out += m;
         n = m;
       }
-      TBG_KLAUNCH(k_l0_final, dim3(1), dim3(kBlock), st, B, in, n);
+      launch_l0_final(B, in, n, st);
       TBG_KLAUNCH(k_l0_after, grid_for(n_groups), dim3(kBlock), st, B);
       // level 0 failed: the group levels' signature side (these kernels
       // return at once after a pass)
@@ -924,7 +944,7 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     } else {
       launch_groups_miller_hex(B, st);
     }
-    TBG_KLAUNCH(k_rlc_group_final, grid_for(fp12_threads(n_groups)), dim3(kBlock), st, B);
+    TBG_KLAUNCH(k_rlc_group_final, grid_for(hex_threads(n_groups)), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
     if (B.rlc_group > 1) {
       // level 1g before the chunks: its unresolved groups add to the chunk list
@@ -933,30 +953,30 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
       TBG_KLAUNCH(k_rlc_gident_lines, grid_for(n_groups * W), dim3(kBlock), st, B);
       fb_passes(B, n_groups, [&](const DevBatch& P, uint32_t n) {
         launch_lines_fold(P, FOLD_GID, n, st);
-        TBG_KLAUNCH(k_rlc_gident_miller, grid_for(fp12_threads(n * (nch + 1))), dim3(kBlock), st, P);
-        TBG_KLAUNCH(k_rlc_gident_check, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+        TBG_KLAUNCH(k_rlc_gident_miller, grid_for(hex_threads(n * (nch + 1))), dim3(kBlock), st, P);
+        TBG_KLAUNCH(k_rlc_gident_check, grid_for(hex_threads(n)), dim3(kBlock), st, P);
       });
       TBG_KLAUNCH(k_rlc_chunk_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
       fb_passes(B, n_groups * nch, [&](const DevBatch& P, uint32_t n) {
         launch_lines_fold(P, FOLD_CHUNKS, n, st);
-        TBG_KLAUNCH(k_rlc_check_chunks, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+        TBG_KLAUNCH(k_rlc_check_chunks, grid_for(hex_threads(n)), dim3(kBlock), st, P);
       });
       TBG_KLAUNCH(k_rlc_cident_lines, grid_for(n_groups * nch), dim3(kBlock), st, B);
       fb_passes(B, n_groups * nch, [&](const DevBatch& P, uint32_t n) {
         launch_lines_fold(P, FOLD_CID, n, st);
-        TBG_KLAUNCH(k_rlc_cident_check, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+        TBG_KLAUNCH(k_rlc_cident_check, grid_for(hex_threads(n)), dim3(kBlock), st, P);
       });
       TBG_KLAUNCH(k_rlc_ident_lines, grid_for(B.n_duties), dim3(kBlock), st, B);
       fb_passes(B, B.n_duties, [&](const DevBatch& P, uint32_t n) {
         launch_lines_fold(P, FOLD_IDENT, n, st);
-        TBG_KLAUNCH(k_rlc_ident_check, grid_for(fp12_threads(n)), dim3(kBlock), st, P);
+        TBG_KLAUNCH(k_rlc_ident_check, grid_for(hex_threads(n)), dim3(kBlock), st, P);
       });
     }
   }
   if (B.n_partials) {
     fb_passes(B, B.n_partials, [&](const DevBatch& P, uint32_t n) {
       TBG_KLAUNCH(k_lines_sig_list, grid_for(n), dim3(kBlock), st, P);
-      TBG_KLAUNCH(k_verify_list, grid_for(fp12_threads(n)), dim3(kBlock), st, P, pk_aff);
+      TBG_KLAUNCH(k_verify_list, grid_for(hex_threads(n)), dim3(kBlock), st, P, pk_aff);
     });
   }
 }

@@ -6,6 +6,8 @@
 // (TBG_BOUNDS_CHECK) switched on.
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
+#include <cstdlib>
 #include "../../charon_amd/csrc/bls_pairing.h"
 #include "../../charon_amd/csrc/bls_h2c.h"
 
@@ -958,5 +960,75 @@ void hc_wide_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   WideHostExec ex;
   wide_mul_to(ex, S, 0, 1, 2);
   f12_out(wide_store(S.v[0]), out);
+}
+}
+
+#include "../../charon_amd/csrc/bls_row.h"
+// Row Fp (bls_row.h): the row algorithms themselves, the row held whole on
+// the host.  Limbs in and out as 14 signed 32-bit values.
+extern "C" {
+static R32 row_in(const int32_t* l) {
+  R32 r;
+  for (int k = 0; k < ROW_N; ++k) r.v[k] = k < NL ? l[k] : 0;
+  return r;
+}
+static void row_out(const R32& r, int32_t* l) {
+  for (int k = 0; k < NL; ++k) l[k] = r.v[k];
+}
+// returns the largest |limb| of the result (and checks lanes 14, 15 stay 0)
+int hc_row_mul2(const int32_t* a, const int32_t* b, const int32_t* c, const int32_t* d, int32_t* out) {
+  const R32 r = row_mul2(row_in(a), row_in(b), row_in(c), row_in(d));
+  row_out(r, out);
+  if (r.v[14] != 0 || r.v[15] != 0) return -1;
+  int32_t mx = 0;
+  for (int k = 0; k < NL - 1; ++k) mx = std::max(mx, std::abs(r.v[k]));
+  return mx;
+}
+int hc_row_mul(const int32_t* a, const int32_t* b, int32_t* out) {
+  const R32 r = row_mul(row_in(a), row_in(b));
+  row_out(r, out);
+  return (r.v[14] != 0 || r.v[15] != 0) ? -1 : 0;
+}
+void hc_row_reduce(const int32_t* a, int32_t* out) { row_out(row_reduce(r_norm(row_in(a))), out); }
+void hc_row_norm(const int32_t* a, int32_t* out) { row_out(r_norm(row_in(a)), out); }
+}
+struct RowHostExec {
+  template <class Fn>
+  void operator()(Fn&& fn) {
+    for (int r = 0; r < 64; ++r) fn(r);
+  }
+};
+struct RowHostSolo {
+  template <class Fn>
+  void operator()(Fn&& fn) { fn(); }
+};
+static RowSlots g_rs;
+extern "C" {
+void hc_row_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  RowHostExec ex;
+  row_scatter(g_rs.v[1], f12_in(a));
+  row_scatter(g_rs.v[2], f12_in(b));
+  row_mul_to(ex, g_rs, 0, 1, 2);
+  f12_out(row_gather(g_rs.v[0]), out);
+}
+void hc_row_fp12_cyc(const uint8_t* a, uint8_t* out) {
+  RowHostExec ex;
+  row_scatter(g_rs.v[0], f12_in(a));
+  row_cyc_sqr(ex, g_rs, 0);
+  f12_out(row_gather(g_rs.v[0]), out);
+}
+void hc_row_fp12_frob(const uint8_t* a, uint8_t* out) {
+  RowHostExec ex;
+  row_scatter(g_rs.v[1], f12_in(a));
+  ex([&](int r) { row_frob(r, g_rs.v[0], g_rs.v[1]); });
+  f12_out(row_gather(g_rs.v[0]), out);
+}
+int hc_row_final_exp(const uint8_t* a, uint8_t* out) {
+  RowHostExec ex;
+  RowHostSolo solo;
+  row_scatter(g_rs.v[0], f12_in(a));
+  row_final_exp(ex, solo, g_rs);
+  f12_out(row_gather(g_rs.v[0]), out);
+  return row_is_one(g_rs.v[0]) ? 1 : 0;
 }
 }

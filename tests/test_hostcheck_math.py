@@ -483,3 +483,82 @@ def test_wide_fp12_final_exp_matches_oracle():
     a, b = rand_f12(), rand_f12()
     assert b2f12(call("hc_wide_mul", f12b(a), f12b(b), out=576)) == bls.f12_mul(a, b)
     assert b2f12(call("hc_wide_final_exp", f12b(a), out=576)) == bls.final_exp(a)
+
+
+def _val(l):
+    return sum(v << (28 * j) for j, v in enumerate(l))
+
+
+def _i32(l):
+    import ctypes
+    return (ctypes.c_int32 * 14)(*l)
+
+
+def _redundant(x):
+    """x with every limb but the top shifted by a random signed amount
+    carried into the next limb (same value, |limb| < 2^29)."""
+    l = [(x >> (28 * j)) & ((1 << 28) - 1) for j in range(13)] + [x >> (28 * 13)]
+    for j in range(13):
+        d = rng.randrange(-3, 4)
+        l[j] += d << 28
+        l[j + 1] -= d
+    return l
+
+
+def test_row_fp_product_and_reduction():
+    """bls_row.h: REDC(a b + c d) with one limb column per lane of a 16-lane
+    row (signed redundant limbs, ds_swizzle broadcasts and DPP shifts run as
+    array operations on the host) equals the oracle's Montgomery product;
+    the reduction brings a value into (-p, 2p) with the same residue."""
+    import ctypes
+    Rinv = pow(1 << 392, -1, P)
+    out = (ctypes.c_int32 * 14)()
+    for trial in range(60):
+        vals = [rng.randrange(P) for _ in range(4)]
+        if trial < 8:
+            vals = [EDGE[trial % len(EDGE)] % P, P - 1, 0, 1][: 4]
+        neg = trial % 3 == 1
+        ls = [_redundant(v) for v in vals]
+        if neg:  # signed inputs: -a, -d
+            ls[0] = [-v for v in ls[0]]
+            ls[3] = [-v for v in ls[3]]
+        a, b, c, d = (_val(l) for l in ls)
+        mx = lib().hc_row_mul2(_i32(ls[0]), _i32(ls[1]), _i32(ls[2]), _i32(ls[3]), out)
+        got = _val(list(out))
+        assert mx >= 0 and mx <= (1 << 28)
+        assert (got - (a * b + c * d) * Rinv) % P == 0
+        assert -P < got < 2 * P
+        lib().hc_row_mul(_i32(ls[0]), _i32(ls[1]), out)
+        got1 = _val(list(out))
+        assert (got1 - a * b * Rinv) % P == 0 and -P < got1 < 2 * P
+    for _ in range(40):
+        x = rng.randrange(-(1 << 388), 1 << 388)
+        l = [(abs(x) >> (28 * j)) & ((1 << 28) - 1) for j in range(13)] + [abs(x) >> (28 * 13)]
+        if x < 0:
+            l = [-v for v in l]
+        lib().hc_row_reduce(_i32(l), out)
+        got = _val(list(out))
+        assert (got - x) % P == 0 and -P < got < 2 * P, (x, got)
+
+
+def test_row_fp12_final_exp_matches_oracle():
+    """bls_row.h Fp12 on rows (k_l0_final's layout: one Fp per 16-lane row,
+    products on 36 rows, phases as bls_wide.h's), rows emulated in turn:
+    product, cyclotomic squaring, Frobenius and the whole final
+    exponentiation equal the oracle's; a cancelling pairing product
+    exponentiates to 1."""
+    import ctypes
+    a, b = rand_f12(), rand_f12()
+    assert b2f12(call("hc_row_fp12_mul", f12b(a), f12b(b), out=576)) == bls.f12_mul(a, b)
+    assert b2f12(call("hc_row_fp12_frob", f12b(a), out=576)) == bls.f12_frob_n(a, 1)
+    f = bls.f12_mul(bls.f12_conj(a), bls.f12_inv(a))
+    f = bls.f12_mul(bls.f12_frob_n(f, 2), f)
+    assert b2f12(call("hc_row_fp12_cyc", f12b(f), out=576)) == bls.f12_sqr(f)
+    out = ctypes.create_string_buffer(576)
+    assert lib().hc_row_final_exp(f12b(a), out) == 0
+    assert b2f12(out.raw) == bls.final_exp(a)
+    p = bls.g1_mul(bls.G1_GEN, rng.randrange(1, bls.R))
+    q = bls.g2_mul(bls.G2_GEN, rng.randrange(1, bls.R))
+    m1 = b2f12(call("hc_miller", be(p[0]) + be(p[1]), aff2b(q), out=576))
+    m2 = b2f12(call("hc_miller", be(p[0]) + be((P - p[1]) % P), aff2b(q), out=576))
+    assert lib().hc_row_final_exp(f12b(bls.f12_mul(m1, m2)), out) == 1
