@@ -568,9 +568,137 @@ TBG_HD Fp fp_inv_vartime(const Fp& a) {
   return fp_mul(fp_select(li_is_one(u), x1, x2), fp_from_const(R3_L));
 }
 
+// ---- Bernstein-Yang inversion ("Fast constant-time gcd computation and
+// modular inversion", 2019), variable-time form: divsteps on the low 62 bits
+// of f, g build a 2x2 transition matrix (entries <= 2^62), applied to the
+// full f, g (exact / 2^62) and to the cofactors d, e (/ 2^62 mod p, a
+// Montgomery-style multiple of p making the division exact) -- ~12 batches of
+// 62 steps for 381-bit values instead of ~760 full-width shift / subtract
+// steps.  Integers as seven signed 62-bit limbs (limbs 0..5 in [0, 2^62)).
+struct S62 {
+  int64_t v[7];
+};
+constexpr uint64_t M62 = (1ull << 62) - 1;
+TBG_HD S62 s62_from_fp(const Fp& a) {  // a: normalised limbs, value < 2^392
+  S62 r = {{0, 0, 0, 0, 0, 0, 0}};
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int pos = 28 * i, w = pos / 62, off = pos % 62;
+    const uint64_t x = a.l[i];
+    r.v[w] += (int64_t)((x << off) & M62);
+    if (off + 28 > 62) r.v[w + 1] += (int64_t)(x >> (62 - off));
+  }
+  return r;
+}
+// x >= 0 with normalised limbs -> 14 x 28-bit limbs
+TBG_HD Fp fp_from_s62(const S62& x) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int pos = 28 * i, w = pos / 62, off = pos % 62;
+    uint64_t bits = (uint64_t)x.v[w] >> off;
+    if (off + 28 > 62 && w + 1 < 7) bits |= (uint64_t)x.v[w + 1] << (62 - off);
+    r.l[i] = (uint32_t)(bits & LMASK);
+  }
+  return r;
+}
+// 62 divsteps (delta, f, g) on the low bits; [f_62; g_62] 2^62 = [u v; q r] [f; g]
+TBG_HD int64_t divsteps62(int64_t delta, uint64_t f0, uint64_t g0, int64_t& u, int64_t& v, int64_t& q, int64_t& r) {
+  u = 1;
+  v = 0;
+  q = 0;
+  r = 1;
+#pragma unroll 2
+  for (int i = 0; i < 62; ++i) {
+    const bool godd = (g0 & 1u) != 0, swap = delta > 0 && godd;
+    const uint64_t nf = swap ? g0 : f0;
+    const uint64_t ng = swap ? g0 - f0 : (godd ? g0 + f0 : g0);
+    const int64_t nu = swap ? q : u, nv = swap ? r : v;
+    const int64_t nq = swap ? q - u : (godd ? q + u : q), nr = swap ? r - v : (godd ? r + v : r);
+    f0 = nf;
+    g0 = ng >> 1;
+    u = 2 * nu;
+    v = 2 * nv;
+    q = nq;
+    r = nr;
+    delta = swap ? 1 - delta : 1 + delta;
+  }
+  return delta;
+}
+// (a, b) <- ([m00 m01; m10 m11] (a, b) + (k0, k1) P) / 2^62, exact; P = null: no multiple
+TBG_HD void s62_update(S62& a, S62& b, int64_t m00, int64_t m01, int64_t m10, int64_t m11, const S62* P,
+                       uint64_t pinv) {
+  int64_t k0 = 0, k1 = 0;
+  if (P) {
+    const uint64_t l0 = (uint64_t)m00 * (uint64_t)a.v[0] + (uint64_t)m01 * (uint64_t)b.v[0];
+    const uint64_t l1 = (uint64_t)m10 * (uint64_t)a.v[0] + (uint64_t)m11 * (uint64_t)b.v[0];
+    k0 = (int64_t)((0 - l0 * pinv) & M62);
+    k1 = (int64_t)((0 - l1 * pinv) & M62);
+  }
+  __int128 c0 = (__int128)m00 * a.v[0] + (__int128)m01 * b.v[0];
+  __int128 c1 = (__int128)m10 * a.v[0] + (__int128)m11 * b.v[0];
+  if (P) {
+    c0 += (__int128)k0 * P->v[0];
+    c1 += (__int128)k1 * P->v[0];
+  }
+  c0 >>= 62;  // (the low 62 bits are zero)
+  c1 >>= 62;
+#pragma unroll
+  for (int i = 1; i < 7; ++i) {
+    c0 += (__int128)m00 * a.v[i] + (__int128)m01 * b.v[i];
+    c1 += (__int128)m10 * a.v[i] + (__int128)m11 * b.v[i];
+    if (P) {
+      c0 += (__int128)k0 * P->v[i];
+      c1 += (__int128)k1 * P->v[i];
+    }
+    a.v[i - 1] = (int64_t)((uint64_t)c0 & M62);
+    b.v[i - 1] = (int64_t)((uint64_t)c1 & M62);
+    c0 >>= 62;
+    c1 >>= 62;
+  }
+  a.v[6] = (int64_t)c0;
+  b.v[6] = (int64_t)c1;
+}
+// 1 / a in Montgomery form (a = xR -> 1/x R), VARIABLE TIME (see
+// fp_inv_vartime); fp_inv(0) = 0
+TBG_HD Fp fp_inv_bgcd(const Fp& a) {
+  const Fp x = fp_canon(a);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) nz |= x.l[i];
+  if (nz == 0) return fp_zero();
+  const S62 P = s62_from_fp(fp_from_const(P_L));
+  uint64_t pinv = (uint64_t)P.v[0];  // p^-1 mod 2^64 by Newton (p odd)
+#pragma unroll
+  for (int i = 0; i < 5; ++i) pinv *= 2 - (uint64_t)P.v[0] * pinv;
+  S62 f = P, g = s62_from_fp(x), d = {{0, 0, 0, 0, 0, 0, 0}}, e = {{1, 0, 0, 0, 0, 0, 0}};
+  int64_t delta = 1;
+  for (int it = 0; it < 40; ++it) {  // <= ~18 batches for 381-bit values
+    int64_t u, v, q, r;
+    delta = divsteps62(delta, (uint64_t)f.v[0], (uint64_t)g.v[0], u, v, q, r);
+    s62_update(f, g, u, v, q, r, nullptr, 0);
+    s62_update(d, e, u, v, q, r, &P, pinv);
+    int64_t gz = 0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) gz |= g.v[i];
+    if (gz == 0) break;
+  }
+  // f = +-1 = d x (mod p): 1/x = sign(f) d; |d| < 41 p, shifted by 64 p into (23 p, 105 p)
+  const bool neg = f.v[6] < 0;
+  S62 y;
+  __int128 c = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    c += (__int128)(neg ? -d.v[i] : d.v[i]) + (__int128)64 * P.v[i];
+    y.v[i] = i < 6 ? (int64_t)((uint64_t)c & M62) : (int64_t)c;
+    c >>= 62;
+  }
+  return fp_mul(fp_reduce(fp_from_s62(y)), fp_from_const(R3_L));
+}
+
 // The inversion of every public value (see fp_inv_vartime).  Values that
 // depend on a secret key call fp_inv_fermat directly (k_gen.hip).
-TBG_HD Fp fp_inv(const Fp& a) { return fp_inv_vartime(a); }
+TBG_HD Fp fp_inv(const Fp& a) { return fp_inv_bgcd(a); }
 
 // Big-endian bytes (48) -> integer limbs; also reports whether value < p.
 TBG_HD Fp fp_limbs_from_be48(const uint8_t* b, bool* lt_p) {

@@ -436,4 +436,184 @@ TBG_HD void row_final_exp(Exec& ex, Solo& solo, RowSlots& S) {
   row_final_exp_inv(ex, S);
 }
 
+#if defined(__HIP__)
+// device: a row phase on every row of the workgroup, then a barrier
+struct RowDevExec {
+  template <class Fn>
+  __device__ void operator()(Fn&& fn) {
+    fn((int)(threadIdx.x >> 4));
+    __syncthreads();
+  }
+};
+#endif
+
+// ---------------------------------------------------------------------------
+// Miller lines of ONE G2 point on rows (level 0's batch-wide S, -g1 folded
+// in: the serial step of every level-0 launch between the bucket MSM and the
+// Miller products).  T = (X, Y, Z) and Q = (x, y) are ten row values; every
+// doubling is three product phases and a combination, every addition five
+// and a combination (miller_dbl_g / miller_add_g's formulas, the Fp2
+// products of a phase on two rows each: c0 and c1).
+struct RowLineSlots {
+  int32_t s[10][16];      // X0 X1 Y0 Y1 Z0 Z1 | x0 x1 y0 y1
+  int32_t p[5][12][16];   // the phases' products
+  int32_t k[2][16];       // nxP, yP
+  int32_t l[2][6][16];    // finished lines (l0, l1, l4), double-buffered
+};
+enum { RL_X = 0, RL_Y = 2, RL_Z = 4, RL_QX = 6, RL_QY = 8 };
+TBG_HD R32 rl_ld(const RowLineSlots& S, int i) { return row_ld(S.s[i]); }
+TBG_HD R32 rl_p(const RowLineSlots& S, int ph, int i) { return row_ld(S.p[ph][i]); }
+// product job: rows 2 j (c0) and 2 j + 1 (c1) of the Fp2 product a b
+TBG_HD void rl_job(RowLineSlots& S, int ph, int r, const R32& a0, const R32& a1, const R32& b0, const R32& b1) {
+  row_st(S.p[ph][r], row_fp2_mul_c(r & 1, a0, a1, b0, b1));
+}
+
+// ---- doubling T <- 2T and its line
+TBG_HD void rl_dbl1(int r, RowLineSlots& S) {  // A = X^2, B = Y^2, ZZ = Z^2, YZ = Y Z
+  if (r >= 8) return;
+  const int j = r >> 1;
+  const int ia = j == 0 ? RL_X : (j == 1 ? RL_Y : (j == 2 ? RL_Z : RL_Y));
+  const int ib = j == 0 ? RL_X : (j == 1 ? RL_Y : RL_Z);
+  rl_job(S, 0, r, rl_ld(S, ia), rl_ld(S, ia + 1), rl_ld(S, ib), rl_ld(S, ib + 1));
+}
+TBG_HD void rl_dbl2(int r, RowLineSlots& S) {  // C = B^2, (X + B)^2, F = E^2, X E, ZZ E, 2 YZ ZZ;  E = 3A
+  if (r >= 12) return;
+  const int j = r >> 1;
+  const R32 E0 = r_norm(r_mul_small(rl_p(S, 0, 0), 3)), E1 = r_norm(r_mul_small(rl_p(S, 0, 1), 3));
+  R32 a0, a1, b0, b1;
+  if (j == 0) { a0 = b0 = rl_p(S, 0, 2); a1 = b1 = rl_p(S, 0, 3); }
+  else if (j == 1) { a0 = b0 = rl_ld(S, RL_X) + rl_p(S, 0, 2); a1 = b1 = rl_ld(S, RL_X + 1) + rl_p(S, 0, 3); }
+  else if (j == 2) { a0 = b0 = E0; a1 = b1 = E1; }
+  else if (j == 3) { a0 = rl_ld(S, RL_X); a1 = rl_ld(S, RL_X + 1); b0 = E0; b1 = E1; }
+  else if (j == 4) { a0 = rl_p(S, 0, 4); a1 = rl_p(S, 0, 5); b0 = E0; b1 = E1; }
+  else { a0 = r_mul_small(rl_p(S, 0, 6), 2); a1 = r_mul_small(rl_p(S, 0, 7), 2); b0 = rl_p(S, 0, 4); b1 = rl_p(S, 0, 5); }
+  rl_job(S, 1, r, a0, a1, b0, b1);
+}
+// D = 2((X + B)^2 - A - C), X3 = F - 2D (component c)
+TBG_HD R32 rl_D(const RowLineSlots& S, int c) {
+  return r_norm(r_mul_small(rl_p(S, 1, 2 + c) - rl_p(S, 0, c) - rl_p(S, 1, c), 2));
+}
+TBG_HD R32 rl_X3(const RowLineSlots& S, int c) { return r_norm(rl_p(S, 1, 4 + c) - r_mul_small(rl_D(S, c), 2)); }
+TBG_HD void rl_dbl3(int r, RowLineSlots& S) {  // (D - X3) E, l1 = ZZ E nxP, l4 = 2 YZ ZZ yP
+  if (r >= 6) return;
+  const int j = r >> 1;
+  R32 a0, a1, b0, b1;
+  const R32 z = r_splat(0);
+  if (j == 0) {
+    a0 = r_norm(rl_D(S, 0) - rl_X3(S, 0));
+    a1 = r_norm(rl_D(S, 1) - rl_X3(S, 1));
+    b0 = r_norm(r_mul_small(rl_p(S, 0, 0), 3));
+    b1 = r_norm(r_mul_small(rl_p(S, 0, 1), 3));
+  } else if (j == 1) { a0 = rl_p(S, 1, 8); a1 = rl_p(S, 1, 9); b0 = row_ld(S.k[0]); b1 = z; }
+  else { a0 = rl_p(S, 1, 10); a1 = rl_p(S, 1, 11); b0 = row_ld(S.k[1]); b1 = z; }
+  rl_job(S, 2, r, a0, a1, b0, b1);
+}
+TBG_HD void rl_dbl4(int r, RowLineSlots& S, int buf) {  // new T and the line
+  if (r >= 12) return;
+  const int c = r & 1, j = r >> 1;
+  if (j == 0) row_st(S.s[RL_X + c], row_reduce(rl_X3(S, c)));
+  else if (j == 1) row_st(S.s[RL_Y + c], row_reduce(rl_p(S, 2, c) - r_mul_small(r_norm(r_mul_small(rl_p(S, 1, c), 4)), 2)));
+  else if (j == 2) row_st(S.s[RL_Z + c], row_reduce(r_mul_small(rl_p(S, 0, 6 + c), 2)));
+  else if (j == 3) row_st(S.l[buf][c], row_reduce(rl_p(S, 1, 6 + c) - r_mul_small(rl_p(S, 0, 2 + c), 2)));  // X E - 2B
+  else if (j == 4) row_st(S.l[buf][2 + c], rl_p(S, 2, 2 + c));
+  else row_st(S.l[buf][4 + c], rl_p(S, 2, 4 + c));
+}
+
+// ---- addition T <- T + Q and its line
+TBG_HD void rl_add1(int r, RowLineSlots& S) {  // ZZ = Z^2, yZ = y Z
+  if (r >= 4) return;
+  const int ia = r < 2 ? RL_Z : RL_QY;
+  rl_job(S, 0, r, rl_ld(S, ia), rl_ld(S, ia + 1), rl_ld(S, RL_Z), rl_ld(S, RL_Z + 1));
+}
+TBG_HD void rl_add2(int r, RowLineSlots& S) {  // U2 = x ZZ, S2 = yZ ZZ
+  if (r >= 4) return;
+  const R32 a0 = r < 2 ? rl_ld(S, RL_QX) : rl_p(S, 0, 2), a1 = r < 2 ? rl_ld(S, RL_QX + 1) : rl_p(S, 0, 3);
+  rl_job(S, 1, r, a0, a1, rl_p(S, 0, 0), rl_p(S, 0, 1));
+}
+TBG_HD R32 rl_H(const RowLineSlots& S, int c) { return r_norm(rl_p(S, 1, c) - rl_ld(S, RL_X + c)); }
+TBG_HD R32 rl_R(const RowLineSlots& S, int c) { return r_norm(rl_p(S, 1, 2 + c) - rl_ld(S, RL_Y + c)); }
+TBG_HD void rl_add3(int r, RowLineSlots& S) {  // HH = H^2, Z3 = Z H, RR = R^2, l1 = R nxP
+  if (r >= 8) return;
+  const int j = r >> 1;
+  const R32 z = r_splat(0);
+  R32 a0, a1, b0, b1;
+  if (j == 0) { a0 = b0 = rl_H(S, 0); a1 = b1 = rl_H(S, 1); }
+  else if (j == 1) { a0 = rl_ld(S, RL_Z); a1 = rl_ld(S, RL_Z + 1); b0 = rl_H(S, 0); b1 = rl_H(S, 1); }
+  else if (j == 2) { a0 = b0 = rl_R(S, 0); a1 = b1 = rl_R(S, 1); }
+  else { a0 = rl_R(S, 0); a1 = rl_R(S, 1); b0 = row_ld(S.k[0]); b1 = z; }
+  rl_job(S, 2, r, a0, a1, b0, b1);
+}
+TBG_HD void rl_add4(int r, RowLineSlots& S) {  // HHH = H HH, V = X HH, y Z3, R x, l4 = Z3 yP
+  if (r >= 10) return;
+  const int j = r >> 1;
+  const R32 z = r_splat(0);
+  R32 a0, a1, b0, b1;
+  if (j == 0) { a0 = rl_H(S, 0); a1 = rl_H(S, 1); b0 = rl_p(S, 2, 0); b1 = rl_p(S, 2, 1); }
+  else if (j == 1) { a0 = rl_ld(S, RL_X); a1 = rl_ld(S, RL_X + 1); b0 = rl_p(S, 2, 0); b1 = rl_p(S, 2, 1); }
+  else if (j == 2) { a0 = rl_ld(S, RL_QY); a1 = rl_ld(S, RL_QY + 1); b0 = rl_p(S, 2, 2); b1 = rl_p(S, 2, 3); }
+  else if (j == 3) { a0 = rl_R(S, 0); a1 = rl_R(S, 1); b0 = rl_ld(S, RL_QX); b1 = rl_ld(S, RL_QX + 1); }
+  else { a0 = rl_p(S, 2, 2); a1 = rl_p(S, 2, 3); b0 = row_ld(S.k[1]); b1 = z; }
+  rl_job(S, 3, r, a0, a1, b0, b1);
+}
+// X3 = RR - HHH - 2V
+TBG_HD R32 rl_aX3(const RowLineSlots& S, int c) {
+  return r_norm(rl_p(S, 2, 4 + c) - rl_p(S, 3, c) - r_mul_small(rl_p(S, 3, 2 + c), 2));
+}
+TBG_HD void rl_add5(int r, RowLineSlots& S) {  // Y HHH, (V - X3) R
+  if (r >= 4) return;
+  R32 a0, a1, b0, b1;
+  if (r < 2) { a0 = rl_ld(S, RL_Y); a1 = rl_ld(S, RL_Y + 1); b0 = rl_p(S, 3, 0); b1 = rl_p(S, 3, 1); }
+  else {
+    a0 = r_norm(rl_p(S, 3, 2) - rl_aX3(S, 0));
+    a1 = r_norm(rl_p(S, 3, 3) - rl_aX3(S, 1));
+    b0 = rl_R(S, 0);
+    b1 = rl_R(S, 1);
+  }
+  rl_job(S, 4, r, a0, a1, b0, b1);
+}
+TBG_HD void rl_add6(int r, RowLineSlots& S, int buf) {
+  if (r >= 12) return;
+  const int c = r & 1, j = r >> 1;
+  if (j == 0) row_st(S.s[RL_X + c], row_reduce(rl_aX3(S, c)));
+  else if (j == 1) row_st(S.s[RL_Y + c], row_reduce(rl_p(S, 4, 2 + c) - rl_p(S, 4, c)));
+  else if (j == 2) row_st(S.s[RL_Z + c], rl_p(S, 2, 2 + c));
+  else if (j == 3) row_st(S.l[buf][c], row_reduce(rl_p(S, 3, 6 + c) - rl_p(S, 3, 4 + c)));  // R x - y Z3
+  else if (j == 4) row_st(S.l[buf][2 + c], rl_p(S, 2, 6 + c));
+  else row_st(S.l[buf][4 + c], rl_p(S, 3, 8 + c));
+}
+
+// one finished line to HBM in line_store's order (plain limbs in [0, 2p));
+// `Solo6` runs the six conversions (one Fp each) on one thread apiece
+TBG_HD void rl_line_out(const RowLineSlots& S, int buf, int k, uint32_t* dst) {
+  const Fp v = fp_from_signed(S.l[buf][k]);
+  for (int i = 0; i < NL; ++i) dst[k * NL + i] = v.l[i];
+}
+
+// All 68 lines of Q (affine, plain limbs) with (nxP, yP) folded in, in loop
+// order.  `ex` runs a row phase on every row then synchronises; `out6(buf,
+// idx)` stores line buffer `buf` as line idx (six conversions).
+template <class Exec, class Out>
+TBG_HD void row_g2_lines(Exec& ex, Out& out6, RowLineSlots& S) {
+  int idx = 0, buf = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    ex([&](int r) { rl_dbl1(r, S); });
+    ex([&](int r) { rl_dbl2(r, S); });
+    ex([&](int r) { rl_dbl3(r, S); });
+    ex([&](int r) { rl_dbl4(r, S, buf); });
+    out6(buf, idx++);
+    buf ^= 1;
+    if ((X_ABS >> i) & 1) {
+      ex([&](int r) { rl_add1(r, S); });
+      ex([&](int r) { rl_add2(r, S); });
+      ex([&](int r) { rl_add3(r, S); });
+      ex([&](int r) { rl_add4(r, S); });
+      ex([&](int r) { rl_add5(r, S); });
+      ex([&](int r) { rl_add6(r, S, buf); });
+      out6(buf, idx++);
+      buf ^= 1;
+    }
+  }
+}
+
 }  // namespace tbg

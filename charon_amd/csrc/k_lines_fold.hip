@@ -16,10 +16,9 @@ namespace tbg {
 
 template <int KIND>
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
-  if (KIND == FOLD_L0) TBG_URGENT();  // the one S of a level-0 launch: on its critical path
   // both lanes of a pair take the same branches; the fallback kinds run in
   // passes of fb_window list positions from fb_base (launch_rlc_check)
-  const uint32_t k = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + (KIND == FOLD_GROUPS || KIND == FOLD_L0 ? 0u : B.fb_base);
+  const uint32_t k = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + (KIND == FOLD_GROUPS ? 0u : B.fb_base);
   uint32_t* out;
   if (KIND == FOLD_GROUPS) {
     if (k >= (B.n_duties + B.rlc_group - 1) / B.rlc_group || B.grp_state[k] != GRP_LINES) return;
@@ -33,14 +32,9 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
   } else if (KIND == FOLD_GID) {
     if (k >= B.counters[CNT_GID] || !fb_in_pass(B, k) || (B.gid_list[k] & ID_DEGENERATE)) return;
     out = B.gid_lines;
-  } else if (KIND == FOLD_IDENT) {
+  } else {  // FOLD_IDENT
     if (k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k) || (B.id_list[k] & ID_DEGENERATE)) return;
     out = B.id_lines;
-  } else {  // FOLD_L0: level 0's S (k_msm_tree_final)
-    if (k != 0 || B.counters[CNT_L0_BAD]) return;
-    const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-    px_g2_lines(px_load(*B.batch_pt), nx, fp_from_const(G1_NEG_Y), B.batch_lines);
-    return;
   }
   const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
   px_g2_lines(px_load(B.pend_pts[k]), nx, fp_from_const(G1_NEG_Y),
@@ -54,7 +48,6 @@ void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStr
     case FOLD_GROUPS: TBG_KLAUNCH(k_lines_fold<FOLD_GROUPS>, grid, dim3(kBlock), st, B); break;
     case FOLD_CHUNKS: TBG_KLAUNCH(k_lines_fold<FOLD_CHUNKS>, grid, dim3(kBlock), st, B); break;
     case FOLD_CID: TBG_KLAUNCH(k_lines_fold<FOLD_CID>, grid, dim3(kBlock), st, B); break;
-    case FOLD_L0: TBG_KLAUNCH(k_lines_fold<FOLD_L0>, grid, dim3(kBlock), st, B); break;
     case FOLD_GID: TBG_KLAUNCH(k_lines_fold<FOLD_GID>, grid, dim3(kBlock), st, B); break;
     default: TBG_KLAUNCH(k_lines_fold<FOLD_IDENT>, grid, dim3(kBlock), st, B); break;
   }

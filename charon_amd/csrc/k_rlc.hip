@@ -30,13 +30,15 @@
 // The P == Q case of the mixed addition doubles inline (bls_curve.h): no
 // out-of-line call inside the kernels' point loops.
 #define TBG_ADD_DBL_INLINE 1
+#ifndef TBG_SCHED_FENCE
+#define TBG_SCHED_FENCE 1  // products in program order (bls_field.h): keeps the tower inverse inside the hexad kernels' budget
+#endif
 #include "tbls_launch.h"
 #include "bls_h2c.h"
 #include "bls_lines.h"
 #include "bls_hex.h"
 #include "bls_rlc.h"
 #include "bls_batchinv.h"
-#include "bls_wide.h"
 #include "bls_row.h"
 
 namespace tbg {
@@ -236,26 +238,13 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_l0_tree(DevBatch B, uint32_t in, u
 
 // The last <= L0_TREE_FAN values times the S pair's product, one final
 // exponentiation for the whole batch -- the latency tail of every level-0
-// launch.  TBG_L0_FINAL selects its layout:
-//   2 (default) on ROWS (bls_row.h: one Fp per 16-lane row, each Montgomery
-//     product limb-parallel over its row): k_l0_final forms f, k_l0_inv
-//     inverts it on one lane (the tower inverse; its out-of-line calls would
-//     pin the row kernel's 576 threads to their register budget), k_l0_fe
-//     exponentiates;
-//   1 on ONE hexad (bls_hex.h);
-//   0 over the lanes of one wave (bls_wide.h: one Fp product per lane).
-#ifndef TBG_L0_FINAL
-#define TBG_L0_FINAL 2
-#endif
-#if TBG_L0_FINAL == 2
+// launch -- on ROWS (bls_row.h: one Fp per 16-lane row, each Montgomery
+// product limb-parallel over its row): k_l0_final forms f, k_l0_inv inverts
+// it on one lane (the tower inverse; its out-of-line calls would pin the row
+// kernel's 576 threads to their register budget), k_l0_fe exponentiates.
+// 1.1 ms per launch against 3.3 ms on a hexad (bls_hex.h) or spread over one
+// wave with one Fp product per lane (round 3; profiles/r04/rowfe/).
 constexpr uint32_t L0_FINAL_THREADS = 16 * 36;  // 36 rows: a product step's Fp products
-struct RowDevExec {
-  template <class Fn>
-  __device__ void operator()(Fn&& fn) {
-    fn((int)(threadIdx.x >> 4));
-    __syncthreads();
-  }
-};
 // f and f^-1 between the three kernels: two spare grp_f entries (12 x 14
 // signed limbs each, the row words; grp_f_entries keeps 40 spare)
 __device__ __forceinline__ int32_t* l0_f_spare(const DevBatch& B, int k) {
@@ -313,54 +302,40 @@ __global__ void __launch_bounds__(L0_FINAL_THREADS) k_l0_fe(DevBatch B) {
   row_final_exp_inv(ex, S);
   if (threadIdx.x == 0 && row_is_one(S.v[0])) B.counters[CNT_L0_OK] = 1;
 }
+// Level 0's S lines (-g1 folded in) on rows: 12 rows, the six conversions of
+// each finished line to HBM on row 8's first lanes (idle in the first phase
+// of the next step).  On one lane pair (k_lines_fold) this was 1.4 ms of the
+// launch's serial path.
+constexpr uint32_t L0_LINES_THREADS = 16 * 12;
+__global__ void __launch_bounds__(L0_LINES_THREADS) k_l0_lines(DevBatch B) {
+  TBG_URGENT();
+  if (B.counters[CNT_L0_BAD]) return;  // (workgroup-uniform)
+  __shared__ RowLineSlots S;
+  RowDevExec ex;
+  const int r = threadIdx.x >> 4;
+  ex([&](int) {
+    const G2A& Q = *B.batch_pt;
+    const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X))), y = fp_from_const(G1_NEG_Y);
+    const Fp* c[12] = {&Q.x.c0, &Q.x.c1, &Q.y.c0, &Q.y.c1, nullptr, nullptr, &Q.x.c0, &Q.x.c1, &Q.y.c0, &Q.y.c1, &nx, &y};
+    const Fp one = fp_one(), zero = fp_zero();
+    const Fp* v = r == 4 ? &one : (r == 5 ? &zero : c[r]);
+    row_st(r < 10 ? S.s[r] : S.k[r - 10], row_from_limbs(v->l));
+  });
+  auto out6 = [&](int buf, int idx) {
+    const int t = (int)threadIdx.x - 128;
+    if (t >= 0 && t < 6) rl_line_out(S, buf, t, B.batch_lines + (size_t)LINE_WORDS * idx);
+  };
+  row_g2_lines(ex, out6, S);
+}
+void launch_l0_lines(const DevBatch& B, hipStream_t st) {
+  TBG_KLAUNCH(k_l0_lines, dim3(1), dim3(L0_LINES_THREADS), st, B);
+}
+
 static void launch_l0_final(const DevBatch& B, uint32_t in, uint32_t n, hipStream_t st) {
   TBG_KLAUNCH(k_l0_final, dim3(1), dim3(L0_FINAL_THREADS), st, B, in, n);
   TBG_KLAUNCH(k_l0_inv, dim3(1), dim3(64), st, B);
   TBG_KLAUNCH(k_l0_fe, dim3(1), dim3(L0_FINAL_THREADS), st, B);
 }
-#elif TBG_L0_FINAL == 1
-__global__ void __launch_bounds__(64) k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
-  TBG_URGENT();
-  if (B.counters[CNT_L0_BAD] || hex_slot(threadIdx.x) != 0) return;  // (one hexad: lanes 0..2, 16..18)
-  Fp4h f = hex_load(B.batch_f);
-  for (uint32_t a = 0; a < n; ++a) f = hex_mul_ni(f, hex_load(B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)));
-  f = hex_final_exp_in(f);
-  if (hex_is_one(f) && hex_lead()) B.counters[CNT_L0_OK] = 1;
-}
-static void launch_l0_final(const DevBatch& B, uint32_t in, uint32_t n, hipStream_t st) {
-  TBG_KLAUNCH(k_l0_final, dim3(1), dim3(64), st, B, in, n);
-}
-#else
-struct WideDevExec {
-  template <class Fn>
-  __device__ void operator()(Fn&& fn) {
-    fn((int)threadIdx.x);
-    __syncthreads();
-  }
-};
-__global__ void __launch_bounds__(64) k_l0_final(DevBatch B, uint32_t in, uint32_t n) {
-  TBG_URGENT();
-  if (B.counters[CNT_L0_BAD]) return;  // (workgroup-uniform)
-  __shared__ WideSlots S;
-  WideDevExec ex;
-  const int l = threadIdx.x;
-  // quad layout in HBM: Fp v of A_q at (4 q + k) NL -- the wide order
-  auto load = [&](int slot, const uint32_t* src) {
-    if (l < WIDE_FP)
-      for (int j = 0; j < NL; ++j) S.v[slot][l].l[j] = src[l * NL + j];
-  };
-  ex([&](int) { load(0, B.batch_f); });
-  for (uint32_t a = 0; a < n; ++a) {
-    ex([&](int) { load(1, B.grp_f + (size_t)3 * QUAD_WORDS * (in + a)); });
-    wide_mul_to(ex, S, 0, 0, 1);
-  }
-  wide_final_exp(ex, S);
-  if (l == 0 && wide_is_one(S.v[0])) B.counters[CNT_L0_OK] = 1;
-}
-static void launch_l0_final(const DevBatch& B, uint32_t in, uint32_t n, hipStream_t st) {
-  TBG_KLAUNCH(k_l0_final, dim3(1), dim3(64), st, B, in, n);
-}
-#endif
 
 // One thread per group: after a level-0 pass every group with a combined
 // duty is accepted (k_rlc_resolve_groups marks its candidates valid).
@@ -902,7 +877,7 @@ void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff
     if (after_keys) after_keys(B, st);
     launch_l0_msm(B, st);
     TBG_KLAUNCH(k_rlc_duty_sum<DSUM_L0_P>, duty_grid(B), dim3(BINV_BLOCK), st, B);
-    launch_lines_fold(B, FOLD_L0, 1, st);
+    launch_l0_lines(B, st);
     return;
   }
   if (after_keys) after_keys(B, st);

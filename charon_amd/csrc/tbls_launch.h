@@ -169,7 +169,7 @@ enum DutySumPhase : int { DSUM_BOTH = 0, DSUM_L0_P = 1, DSUM_FALLBACK_S = 2 };
 constexpr uint32_t CHUNK_DEGENERATE = 0x80000000u;
 constexpr uint32_t ID_DEGENERATE = 0x80000000u;
 // k_lines_fold<KIND>: which pending points get lines, and where they go.
-enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3, FOLD_L0 = 4, FOLD_GID = 5 };
+enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT = 3, FOLD_GID = 5 };
 
 // Fallback list position k in the current pass, and its slot in the line buffer.
 TBG_HD bool fb_in_pass(const DevBatch& B, uint32_t k) { return B.fb_window == 0 || k - B.fb_base < B.fb_window; }

@@ -416,7 +416,16 @@ static H6 frob(const H6& A) {
     for (uint32_t c = 0; c < 2; ++c) R.v[q][c] = hx_frob(c, q, A.v[q][c], A.v[q][c ^ 1]);
   return R;
 }
-static H6 inv(const H6& A) { return split(fp12_inv(join(A))); }
+// hex_inv: conj(f) (f conj(f))^-1 with the Fp6 inverse of the gathered norm
+static H6 inv(const H6& A) {
+  const H6 C = conj(A), N = mul(A, C);
+  const Fp12 n = join(N);
+  const Fp6 r = fp6_inv_in(n.c0);
+  H6 R;
+  for (int q = 0; q < 3; ++q)
+    for (uint32_t c = 0; c < 2; ++c) R.v[q][c] = hx_inv_scatter(c, q, r);
+  return mul(C, R);
+}
 static bool is_one(const H6& A) {
   bool ok = true;
   for (int q = 0; q < 3; ++q)
@@ -938,30 +947,6 @@ void hc_batch_inv_cost(int n, int waves) {
 }
 }  // extern "C"
 
-#include "../../charon_amd/csrc/bls_wide.h"
-// The wave-wide Fp12 of bls_wide.h (k_l0_final's final exponentiation),
-// lanes emulated phase by phase: FE of a, and a * b.
-extern "C" {
-static void wide_load(tbg::Fp* v, const Fp12& f) {
-  for (int q = 0; q < 3; ++q) wide_put4(v, q, quad_from_fp12(q, f));
-}
-static Fp12 wide_store(const tbg::Fp* v) { return quad_to_fp12(wide_fp4(v, 0), wide_fp4(v, 1), wide_fp4(v, 2)); }
-void hc_wide_final_exp(const uint8_t* a, uint8_t* out) {
-  static WideSlots S;
-  wide_load(S.v[0], f12_in(a));
-  WideHostExec ex;
-  wide_final_exp(ex, S);
-  f12_out(wide_store(S.v[0]), out);
-}
-void hc_wide_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
-  static WideSlots S;
-  wide_load(S.v[1], f12_in(a));
-  wide_load(S.v[2], f12_in(b));
-  WideHostExec ex;
-  wide_mul_to(ex, S, 0, 1, 2);
-  f12_out(wide_store(S.v[0]), out);
-}
-}
 
 #include "../../charon_amd/csrc/bls_row.h"
 // Row Fp (bls_row.h): the row algorithms themselves, the row held whole on
@@ -1030,5 +1015,41 @@ int hc_row_final_exp(const uint8_t* a, uint8_t* out) {
   row_final_exp(ex, solo, g_rs);
   f12_out(row_gather(g_rs.v[0]), out);
   return row_is_one(g_rs.v[0]) ? 1 : 0;
+}
+}
+extern "C" {
+// Bernstein-Yang inversion against Fermat: 0 on agreement
+int hc_inv_bgcd(const uint8_t* a48, uint8_t* out48) {
+  const Fp a = from_be(a48);
+  const Fp r = fp_inv_bgcd(a), f = fp_inv_fermat(a);
+  to_be(fp_canon(r), out48);
+  return fp_eq(r, f) ? 0 : 1;
+}
+}
+extern "C" {
+// The 68 -g1-folded lines of an affine G2 point (4 x 48-byte coordinates,
+// x.c0 x.c1 y.c0 y.c1) on rows (bls_row.h) against g2_lines: mismatching Fp count
+int hc_row_lines(const uint8_t* q192) {
+  static RowLineSlots S;
+  static uint32_t ref[LINES_WORDS], got[LINES_WORDS];
+  G2A Q{{from_be(q192), from_be(q192 + 48)}, {from_be(q192 + 96), from_be(q192 + 144)}};
+  const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X))), y = fp_from_const(G1_NEG_Y);
+  g2_lines(Q, nx, y, ref);
+  const Fp c[10] = {Q.x.c0, Q.x.c1, Q.y.c0, Q.y.c1, fp_one(), fp_zero(), Q.x.c0, Q.x.c1, Q.y.c0, Q.y.c1};
+  for (int i = 0; i < 10; ++i) row_st(S.s[i], row_from_limbs(c[i].l));
+  row_st(S.k[0], row_from_limbs(nx.l));
+  row_st(S.k[1], row_from_limbs(y.l));
+  RowHostExec ex;
+  auto out6 = [&](int buf, int idx) {
+    for (int k = 0; k < 6; ++k) rl_line_out(S, buf, k, got + LINE_WORDS * idx);
+  };
+  row_g2_lines(ex, out6, S);
+  int bad = 0;
+  for (int i = 0; i < N_LINES * 6; ++i) {
+    Fp a, b;
+    for (int j = 0; j < NL; ++j) { a.l[j] = ref[i * NL + j]; b.l[j] = got[i * NL + j]; }
+    if (!fp_eq(a, b)) ++bad;
+  }
+  return bad;
 }
 }

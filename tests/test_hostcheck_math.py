@@ -476,15 +476,6 @@ def test_hex_final_exp_pieces_match_tower():
     assert lib().hc_hex_final_exp(f12b(bls.f12_mul(m1, m2)), out) == 1
 
 
-def test_wide_fp12_final_exp_matches_oracle():
-    """bls_wide.h (one Fp12 over a wave's lanes, k_l0_final): the product and
-    the whole final exponentiation, lanes emulated phase by phase, equal the
-    oracle's; a Miller value that passes its check exponentiates to 1."""
-    a, b = rand_f12(), rand_f12()
-    assert b2f12(call("hc_wide_mul", f12b(a), f12b(b), out=576)) == bls.f12_mul(a, b)
-    assert b2f12(call("hc_wide_final_exp", f12b(a), out=576)) == bls.final_exp(a)
-
-
 def _val(l):
     return sum(v << (28 * j) for j, v in enumerate(l))
 
@@ -543,7 +534,7 @@ def test_row_fp_product_and_reduction():
 
 def test_row_fp12_final_exp_matches_oracle():
     """bls_row.h Fp12 on rows (k_l0_final's layout: one Fp per 16-lane row,
-    products on 36 rows, phases as bls_wide.h's), rows emulated in turn:
+    products on 36 rows, a phase per row role), rows emulated in turn:
     product, cyclotomic squaring, Frobenius and the whole final
     exponentiation equal the oracle's; a cancelling pairing product
     exponentiates to 1."""
@@ -562,3 +553,26 @@ def test_row_fp12_final_exp_matches_oracle():
     m1 = b2f12(call("hc_miller", be(p[0]) + be(p[1]), aff2b(q), out=576))
     m2 = b2f12(call("hc_miller", be(p[0]) + be((P - p[1]) % P), aff2b(q), out=576))
     assert lib().hc_row_final_exp(f12b(bls.f12_mul(m1, m2)), out) == 1
+
+
+def test_bernstein_yang_inversion():
+    """fp_inv (bls_field.h, Bernstein-Yang divsteps in 62-bit batches, the
+    inversion of every public value) equals Fermat's and the oracle's inverse
+    on edge values and random ones; 0 maps to 0."""
+    vals = [0, 1, 2, 3, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 1 << 380, (1 << 381) % P, 0xDEADBEEF]
+    vals += [pow(2, k, P) for k in range(0, 381, 37)] + [rng.randrange(P) for _ in range(300)]
+    import ctypes
+    for v in vals:
+        ob = ctypes.create_string_buffer(48)
+        rc = lib().hc_inv_bgcd(be(v), ob)
+        assert rc == 0, v
+        assert fe(ob.raw) == (pow(v, P - 2, P) if v else 0)
+
+
+def test_row_g2_lines_match_lane_lines():
+    """Level 0's S lines on rows (bls_row.h: each Fp2 product of a doubling /
+    addition phase on two 16-lane rows) equal g2_lines's 68 lines, -g1
+    folded in, Fp for Fp."""
+    for _ in range(3):
+        q = bls.g2_mul(bls.G2_GEN, rng.randrange(1, bls.R))
+        assert lib().hc_row_lines(aff2b(q)) == 0

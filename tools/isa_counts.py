@@ -38,12 +38,14 @@ def main():
     ap.add_argument("--defines", nargs="*", default=[])
     ap.add_argument("--out", default="/tmp/isa")
     ap.add_argument("--reuse", action="store_true", help="count existing .s files in --out")
+    ap.add_argument("--min-valu", type=int, default=500, help="skip functions with fewer VALU instructions")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     for u in a.units:
-        s = os.path.join(a.out, u.replace(".hip", ".s"))
+        s = os.path.join(a.out, os.path.basename(u).replace(".hip", ".s"))
+        src = u if os.path.exists(u) else os.path.join(CSRC, u)
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
-               "-Wno-pass-failed", os.path.join(CSRC, u), "-o", s] + ["-D" + d for d in a.defines]
+               "-Wno-pass-failed", "-I", CSRC, src, "-o", s] + ["-D" + d for d in a.defines]
         if not a.reuse or not os.path.exists(s):
             subprocess.check_call(cmd, stderr=subprocess.DEVNULL)
         ks = kernels(open(s).read())
@@ -52,7 +54,7 @@ def main():
         for k, ops in ks.items():
             valu = sum(v for o, v in ops.items() if o.startswith("v_"))
             mad = ops.get("v_mad_u64_u32", 0)
-            if valu < 500:
+            if valu < a.min_valu:
                 continue
             top = ", ".join(f"{o[2:]} {v}" for o, v in ops.most_common(9) if o.startswith("v_") and o != "v_mad_u64_u32")
             print(f"{dm[k].split('(')[0]:45s} valu {valu:6d} mad {mad:6d} ({mad / max(1, valu):.3f})  "
