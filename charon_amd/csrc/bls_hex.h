@@ -163,15 +163,6 @@ TBG_HD Fp4h hx_frob(uint32_t c, int q, const Fp4h& A, const Fp4h& Ap) {
           hx_mul(c, hx_conj_view(c, A.b, Ap.b), hx_const_view(c, gb))};
 }
 
-// f^-1 = conj(f) N^-1 with N = f conj(f) in Fp6 (the w-even coefficients a0,
-// a2, a4 = A0.a, A2.a, A1.b): the Fp6 inverse of N, scattered back as an Fp12
-// with only those coefficients -- this lane's components of it
-TBG_HD Fp4h hx_inv_scatter(uint32_t c, int q, const Fp6& r) {
-  const Fp2 ra = fp2_select(q == 0, r.c0, fp2_select(q == 2, r.c1, fp2_zero()));
-  const Fp2 rb = fp2_select(q == 1, r.c2, fp2_zero());
-  return {fp_select(c != 0, ra.c1, ra.c0), fp_select(c != 0, rb.c1, rb.c0)};
-}
-
 // this lane's part of "the element is 1": b = 0, a = 1 on (q, c) = (0, 0), 0 elsewhere
 TBG_HD bool hx_is_one_lane(uint32_t c, int q, const Fp4h& A) {
   const bool a_one = fp_eq(A.a, fp_one()), a_zero = fp_is_zero(A.a);
@@ -337,21 +328,23 @@ TBG_DEV bool hex_is_one(const Fp4h& A) {
   return (xch_u32<QP_B0>(v) & xch_u32<QP_B1>(v) & xch_u32<QP_B2>(v)) != 0;
 }
 
-// f^-1 = conj(f) (f conj(f))^-1: one product, the Fp6 inverse of the norm
-// gathered on every lane (inline: an out-of-line tower inverse pinned the
-// check kernels to one wave per SIMD), one product (rare: once per final
-// exponentiation)
-TBG_DEV Fp4h hex_inv(const Fp4h& A) {
+// f^-1: the whole element gathered on every lane, the tower inverse, this
+// lane's components back -- out of line (rare: once per final
+// exponentiation).  (Inline, as conj(f) (f conj(f))^-1 with the Fp6 inverse
+// of the norm, the check kernels fit two waves per SIMD and ran 17 % faster
+// alone but 9 % slower in the pipelined 1 %-invalid run; round 4,
+// profiles/r04/hexinv/.)
+__device__ __noinline__ Fp4h hex_inv_ni(const Fp4h& A) {
   const uint32_t c = hex_c();
-  const Fp4h C = hex_conj(A);
-  const Fp4h N = hex_mul(A, C);
-  const Fp4h Np = hx_swap(N);
-  auto whole = [&](const Fp& own, const Fp& par) -> Fp2 {
-    return {fp_select(c != 0, par, own), fp_select(c != 0, own, par)};
+  const Fp4h Ap = hx_swap(A);
+  auto whole = [&](const Fp4h& own, const Fp4h& par) -> Fp4 {
+    return {{fp_select(c != 0, par.a, own.a), fp_select(c != 0, own.a, par.a)},
+            {fp_select(c != 0, par.b, own.b), fp_select(c != 0, own.b, par.b)}};
   };
-  const Fp6 n = {whole(xch<QP_B0>(N.a), xch<QP_B0>(Np.a)), whole(xch<QP_B2>(N.a), xch<QP_B2>(Np.a)),
-                 whole(xch<QP_B1>(N.b), xch<QP_B1>(Np.b))};
-  return hex_mul(C, hx_inv_scatter(c, quad_lane(), fp6_inv_in(n)));
+  const Fp4 A0 = whole(hxch<QP_B0>(A), hxch<QP_B0>(Ap)), A1 = whole(hxch<QP_B1>(A), hxch<QP_B1>(Ap)),
+            A2 = whole(hxch<QP_B2>(A), hxch<QP_B2>(Ap));
+  const Fp4 r = quad_from_fp12(quad_lane(), fp12_inv(quad_to_fp12(A0, A1, A2)));
+  return {fp_select(c != 0, r.a.c1, r.a.c0), fp_select(c != 0, r.b.c1, r.b.c0)};
 }
 
 // a^|x| in the cyclotomic subgroup, and the final exponentiation f^(3 (p^12
@@ -370,7 +363,7 @@ TBG_DEV Fp4h hex_pow_xabs_in(const Fp4h& a) {
 }
 TBG_DEV Fp4h hex_pow_x_in(const Fp4h& a) { return hex_conj(hex_pow_xabs_in(a)); }
 TBG_DEV Fp4h hex_final_exp_in(const Fp4h& f) {
-  Fp4h t = hex_mul_ni(hex_conj(f), hex_inv(f));
+  Fp4h t = hex_mul_ni(hex_conj(f), hex_inv_ni(f));
   t = hex_mul_ni(hex_frob_ni(hex_frob_ni(t)), t);
   Fp4h a = hex_mul_ni(hex_pow_x_in(t), hex_conj(t));
   a = hex_mul_ni(hex_pow_x_in(a), hex_conj(a));

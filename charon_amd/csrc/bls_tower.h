@@ -180,9 +180,7 @@ TBG_HD Fp6 fp6_mul_by_1(const Fp6& a, const Fp2& b1) {
   return {fp2_reduce(fp2_mul_xi(t0)), t1, t2};
 }
 
-// (the kernel-inline form: bls_hex.h's inversion calls it inside the check
-// kernels, whose register budget an out-of-line call would break)
-TBG_HD Fp6 fp6_inv_in(const Fp6& a) {
+TBG_NI Fp6 fp6_inv(const Fp6& a) {
   Fp2 c0 = fp2_reduce(fp2_sub(fp2_sqr(a.c0), fp2_reduce(fp2_mul_xi(fp2_mul(a.c1, a.c2)))));
   Fp2 c1 = fp2_reduce(fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1)));
   Fp2 c2 = fp2_reduce(fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2)));
@@ -190,7 +188,6 @@ TBG_HD Fp6 fp6_inv_in(const Fp6& a) {
   Fp2 ti = fp2_inv(t);
   return {fp2_mul(c0, ti), fp2_mul(c1, ti), fp2_mul(c2, ti)};
 }
-TBG_NI Fp6 fp6_inv(const Fp6& a) { return fp6_inv_in(a); }
 
 // ----------------------------------------------------------------- Fp12
 TBG_HD Fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }

@@ -416,16 +416,7 @@ static H6 frob(const H6& A) {
     for (uint32_t c = 0; c < 2; ++c) R.v[q][c] = hx_frob(c, q, A.v[q][c], A.v[q][c ^ 1]);
   return R;
 }
-// hex_inv: conj(f) (f conj(f))^-1 with the Fp6 inverse of the gathered norm
-static H6 inv(const H6& A) {
-  const H6 C = conj(A), N = mul(A, C);
-  const Fp12 n = join(N);
-  const Fp6 r = fp6_inv_in(n.c0);
-  H6 R;
-  for (int q = 0; q < 3; ++q)
-    for (uint32_t c = 0; c < 2; ++c) R.v[q][c] = hx_inv_scatter(c, q, r);
-  return mul(C, R);
-}
+static H6 inv(const H6& A) { return split(fp12_inv(join(A))); }
 static bool is_one(const H6& A) {
   bool ok = true;
   for (int q = 0; q < 3; ++q)
