@@ -205,10 +205,12 @@ TBG_HD Jac<F> g2_clear_cofactor_g(const Jac<F>& p, bool& exc) {
 }
 
 // Miller steps (bls_pairing.h miller_dbl_in / miller_add_in) for any Fp2
-// representation; f_mulfp multiplies by an Fp scalar component-wise.
+// representation; f_mulfp multiplies by an Fp scalar component-wise.  EVAL =
+// false leaves P out altogether (the H(m) lines: l1, l4 stored unevaluated,
+// no products by the Montgomery one -- 2 of a line's ~17 products per lane).
 template <class F> struct LineG { F l0, l1, l4; };
 
-template <class F>
+template <class F, bool EVAL = true>
 TBG_HD LineG<F> miller_dbl_g(Jac<F>& T, const Fp& nxP, const Fp& yP) {
   F A = f_sqr(T.X);
   F B = f_sqr(T.Y);
@@ -224,13 +226,17 @@ TBG_HD LineG<F> miller_dbl_g(Jac<F>& T, const Fp& nxP, const Fp& yP) {
   F Z3 = f_reduce(f_add_l(YZ, YZ));
   LineG<F> l;
   l.l0 = f_reduce(f_sub_l(f_mul(T.X, E), f_add(B, B)));   // 3X^3 - 2Y^2
-  l.l1 = f_mulfp(f_mul(ZZ, E), nxP);                     // -3X^2 Z^2 xP
-  l.l4 = f_mulfp(f_mul(Z3, ZZ), yP);                     // 2 Y Z^3 yP
+  l.l1 = f_mul(ZZ, E);                                   // -3X^2 Z^2 xP
+  l.l4 = f_mul(Z3, ZZ);                                  // 2 Y Z^3 yP
+  if (EVAL) {
+    l.l1 = f_mulfp(l.l1, nxP);
+    l.l4 = f_mulfp(l.l4, yP);
+  }
   T = {X3, Y3, Z3};
   return l;
 }
 
-template <class F>
+template <class F, bool EVAL = true>
 TBG_HD LineG<F> miller_add_g(Jac<F>& T, const Aff<F>& Q, const Fp& nxP, const Fp& yP) {
   F ZZ = f_sqr(T.Z);
   F U2 = f_mul(Q.x, ZZ);
@@ -245,8 +251,8 @@ TBG_HD LineG<F> miller_add_g(Jac<F>& T, const Aff<F>& Q, const Fp& nxP, const Fp
   F Z3 = f_mul(T.Z, H);
   LineG<F> l;
   l.l0 = f_reduce(f_sub_l(f_mul(R, Q.x), f_mul(Q.y, Z3)));
-  l.l1 = f_mulfp(R, nxP);
-  l.l4 = f_mulfp(Z3, yP);
+  l.l1 = EVAL ? f_mulfp(R, nxP) : R;
+  l.l4 = EVAL ? f_mulfp(Z3, yP) : Z3;
   T = {X3, Y3, Z3};
   return l;
 }
@@ -354,13 +360,15 @@ TBG_DEV void px_line_store(uint32_t* dst, const LineG<Fp2x>& l) {
     for (int i = 0; i < NL; ++i) dst[(2 * k + par) * NL + i] = f[k]->l[i];
 }
 
-// All 68 lines of Q in loop order (g2_lines_t), Fp2 split over the pair.
+// All 68 lines of Q in loop order (g2_lines_t), Fp2 split over the pair;
+// EVAL = false: P left out (nxP, yP unused).
+template <bool EVAL = true>
 TBG_DEV void px_g2_lines(const Aff<Fp2x>& Q, const Fp& nxP, const Fp& yP, uint32_t* out) {
   Jac<Fp2x> T = jac_from_aff(Q);
   int idx = 0;
   for (int i = 62; i >= 0; --i) {
-    px_line_store(out + LINE_WORDS * idx++, miller_dbl_g(T, nxP, yP));
-    if ((X_ABS >> i) & 1) px_line_store(out + LINE_WORDS * idx++, miller_add_g(T, Q, nxP, yP));
+    px_line_store(out + LINE_WORDS * idx++, miller_dbl_g<Fp2x, EVAL>(T, nxP, yP));
+    if ((X_ABS >> i) & 1) px_line_store(out + LINE_WORDS * idx++, miller_add_g<Fp2x, EVAL>(T, Q, nxP, yP));
   }
 }
 

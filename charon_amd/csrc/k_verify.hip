@@ -16,7 +16,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_h(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (m >= B.n_msgs) return;
   if (B.h_status[m] != 0) return;
-  px_g2_lines(px_load(B.h_aff[m]), fp_one(), fp_one(), B.h_lines + (size_t)LINES_WORDS * m);
+  px_g2_lines<false>(px_load(B.h_aff[m]), fp_one(), fp_one(), B.h_lines + (size_t)LINES_WORDS * m);
 }
 
 void launch_h_lines(const DevBatch& B, hipStream_t st) {

@@ -654,7 +654,8 @@ void hc_pair_ops(const uint8_t* a96, const uint8_t* b96, uint8_t* out) {
 // k_lines_h (pair-emulated miller_dbl_g / miller_add_g) against the
 // single-lane g2_lines of the same point, and the pair-emulated cofactor
 // clearing (g2_clear_cofactor_g, k_hash_clear_*) against g2_clear_cofactor:
-// bit 1 lines equal, bit 2 clearing equal (or the doubling exception taken).
+// bit 1 lines equal, bit 2 clearing equal (or the doubling exception taken),
+// bit 4 the unevaluated lines equal.
 int hc_pair_lines_clear(const uint8_t* sig96) {
   G2A q;
   if (g2_decompress_t<true, false>(sig96, q) != DEC_OK) return -1;  // (no subgroup check: E2 points too)
@@ -672,6 +673,17 @@ int hc_pair_lines_clear(const uint8_t* sig96) {
     same(miller_dbl_g(T, nx, y));
     if ((X_ABS >> i) & 1) same(miller_add_g(T, Q, nx, y));
   }
+  // the unevaluated form (k_lines_h, EVAL = false) against P = (1, 1): bit 4
+  g2_lines(q, fp_one(), fp_one(), ref);
+  T = jac_from_aff(Q);
+  idx = 0;
+  const int before = out;
+  out = 1;
+  for (int i = 62; i >= 0; --i) {
+    same(miller_dbl_g<Fp2p, false>(T, nx, y));
+    if ((X_ABS >> i) & 1) same(miller_add_g<Fp2p, false>(T, Q, nx, y));
+  }
+  out = before | (out ? 4 : 0);
   bool exc = false;
   const Jac<Fp2p> c = g2_clear_cofactor_g(Jac<Fp2p>{Q.x, Q.y, f_one<Fp2p>()}, exc);
   const G2J cg{pp_to(c.X), pp_to(c.Y), pp_to(c.Z)};
