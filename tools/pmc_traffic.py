@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel HBM traffic (KB per launch) from the two rocprofv3 PMC passes
-of tools/gpu_round.sh (FETCH_SIZE and WRITE_SIZE in separate runs, as
+of tools/gpu_pmc.sh (driven by tools/gpu_r04_bench.sh) (FETCH_SIZE and WRITE_SIZE in separate runs, as
 MI355X_MICROARCH.md prescribes) -> JSON for profiles/ and bench.py.
 
   python tools/pmc_traffic.py gpurun_out/round profiles/rNN/traffic.json [batches_per_launch]
