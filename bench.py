@@ -467,7 +467,7 @@ def main():
 
     batches, tickets = [], []
     pcie_ms = None
-    if args.rlc_group == 0 and args.verify_mode == 0 and args.inject > 0:
+    if args.verify_mode == 0 and args.inject > 0:
         # the adaptive group size (tbg_config.rlc_group = 0) follows the invalid
         # share of collected batches: one untimed pass puts it in the state a
         # node serving this traffic is in before the resident slots are built

@@ -819,13 +819,18 @@ __global__ void TBG_LAUNCH k_list_all_partials(DevBatch B, const int32_t* pk_sta
   B.part_list[atomicAdd(&B.counters[CNT_PARTIALS], 1u)] = i;
 }
 
-// Level 3 lines: one thread per listed partial, lines of its signature.
-__global__ void TBG_LAUNCH k_lines_sig_list(DevBatch B) {
-  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x + B.fb_base;
+// Level 3 lines: one lane PAIR per listed partial (bls_pair.h, the Fp2
+// coordinates split over the pair), the lines of its signature with -g1
+// folded in.  (One lane per partial: 2.6 ms of latency per 16-batch launch
+// at 1 % invalid against 1.4 ms, profiles/r04/merge/.)
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_sig_list(DevBatch B) {
+  const uint32_t k = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + B.fb_base;  // (pair-uniform branches)
   if (k >= B.counters[CNT_PARTIALS] || !fb_in_pass(B, k)) return;
-  uint32_t i = B.part_list[k];
-  Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  g2_lines_t<true>(B.sig_aff[i], nx, fp_from_const(G1_NEG_Y), B.sig_lines + fb_slot(B, k));
+  const uint32_t i = B.part_list[k];
+  const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+  Aff<Fp2x> q = px_load(B.sig_aff[i]);
+  q = {f_reduce(q.x), f_reduce(q.y)};  // decoded coordinates may be up to 16p (a negated root)
+  px_g2_lines(q, nx, fp_from_const(G1_NEG_Y), B.sig_lines + fb_slot(B, k));
 }
 
 // Level 3 check: one hexad per listed partial, the exact CoreVerify.
@@ -950,7 +955,7 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
   }
   if (B.n_partials) {
     fb_passes(B, B.n_partials, [&](const DevBatch& P, uint32_t n) {
-      TBG_KLAUNCH(k_lines_sig_list, grid_for(n), dim3(kBlock), st, P);
+      TBG_KLAUNCH(k_lines_sig_list, grid_for(2 * n), dim3(kBlock), st, P);
       TBG_KLAUNCH(k_verify_list, grid_for(hex_threads(n)), dim3(kBlock), st, P, pk_aff);
     });
   }
