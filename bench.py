@@ -393,6 +393,8 @@ def main():
     ap.add_argument("--launches", type=int, default=0,
                     help="spread the timed steps over at least this many launches (default: one per slot)")
     ap.add_argument("--verify-mode", type=int, default=0, help="0 = RLC groups with fallback, 1 = per-partial checks")
+    ap.add_argument("--split", type=lambda v: [int(x) for x in v.split(",")], default=None,
+                    help="batches per launch of a plan whose total is that many steps (launch-size experiments)")
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
@@ -492,6 +494,8 @@ def main():
         round-robin over the slots (a prefix of a packed device batch is a
         batch of its own), so a short run still has `inflight` launches
         overlapping instead of a full launch plus a small remainder."""
+        if args.split and sum(args.split) == n and len(args.split) <= len(tickets) and max(args.split) <= M:
+            return [tickets[k] for k in range(len(args.split))], [0 if x == M else x for x in args.split]
         L = max(-(-n // M), min(len(tickets), n), min(args.launches, n))
         base, extra = divmod(n, L)
         ts, ps = [], []
