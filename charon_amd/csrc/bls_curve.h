@@ -353,7 +353,7 @@ TBG_NI int32_t g1_decompress(const uint8_t* b, G1A& out) {
   if (!lt) return DEC_ERR_FIELD;
   Fp x = fp_to_mont(x0);
   Fp rhs = fp_reduce(fp_add(fp_mul(fp_sqr(x), x), fp_from_const(FOUR_M)));
-  Fp y = fp_pow_const<EXP_SQRT_BITS>(rhs, EXP_SQRT_WORDS);
+  Fp y = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS>(rhs);
   if (!fp_eq(fp_sqr(y), rhs)) return DEC_ERR_NOT_ON_CURVE;
   Fp yc = fp_from_mont(y);
   if ((uint32_t)fp_lex_largest_canon(yc) != s_flag) y = fp_reduce(fp_neg(y));

@@ -428,18 +428,27 @@ TBG_HD Fp fp_to_mont(const Fp& a) {
 }
 
 // Exponentiation by a fixed public exponent: MSB-first sliding window of
-// width 3 over the odd powers a, a^3, a^5, a^7 (about 378 squarings + 100
-// products for the 380-bit exponents of p, against 378 + 228 for square and
-// multiply).  The exponent is public and the same in every lane, so the
-// window scan is uniform control flow.
-template <int NBITS, int NW>
-TBG_NI Fp fp_pow_const(const Fp& a, const uint32_t (&w)[NW]) {
+// width WIN over the odd powers a, a^3, ... (about 378 squarings + 98
+// products at width 3, + 83 at width 4, for the 380-bit exponents of p,
+// against 378 + 228 for square and multiply).  The exponent is a template
+// argument (a constant array), so every bit test is a scalar load and the
+// window scan uniform control flow.  Width 4's eight table entries cost
+// registers: k_hash_map's square roots take it (7.2 -> 6.8 ms per 16-batch
+// launch), k_decode_sigs lost 13 % with it and keeps width 3
+// (profiles/r04/pow/).
+template <int NBITS, const uint32_t (&WD)[12], int WIN = 3>
+TBG_NI Fp fp_pow_const(const Fp& a) {
+  static_assert(WIN == 3 || WIN == 4, "window width");
   const Fp a2 = fp_sqr(a);
-  const Fp t1 = a;
-  const Fp t3 = fp_mul(t1, a2);
-  const Fp t5 = fp_mul(t3, a2);
-  const Fp t7 = fp_mul(t5, a2);
-  auto bit = [&](int i) -> uint32_t { return (w[i >> 5] >> (i & 31)) & 1u; };
+  const Fp t1 = a, t3 = fp_mul(t1, a2), t5 = fp_mul(t3, a2), t7 = fp_mul(t5, a2);
+  Fp t9 = t7, t11 = t7, t13 = t7, t15 = t7;
+  if (WIN == 4) {
+    t9 = fp_mul(t7, a2);
+    t11 = fp_mul(t9, a2);
+    t13 = fp_mul(t11, a2);
+    t15 = fp_mul(t13, a2);
+  }
+  auto bit = [&](int i) -> uint32_t { return (WD[i >> 5] >> (i & 31)) & 1u; };
   Fp r = t1;
   bool started = false;
   int i = NBITS - 1;  // top bit is 1
@@ -449,16 +458,19 @@ TBG_NI Fp fp_pow_const(const Fp& a, const uint32_t (&w)[NW]) {
       --i;
       continue;
     }
-    int L = i + 1 < 3 ? i + 1 : 3;
+    int L = i + 1 < WIN ? i + 1 : WIN;
     while (!bit(i - L + 1)) --L;
     uint32_t v = 0;
     for (int k = 0; k < L; ++k) v = (v << 1) | bit(i - k);
-    const Fp t = fp_select(v == 1, t1, fp_select(v == 3, t3, fp_select(v == 5, t5, t7)));
+    Fp tv;
+    if (WIN == 3) tv = fp_select(v == 1, t1, fp_select(v == 3, t3, fp_select(v == 5, t5, t7)));
+    else if (v < 9) tv = v < 5 ? (v == 1 ? t1 : t3) : (v == 5 ? t5 : t7);
+    else tv = v < 13 ? (v == 9 ? t9 : t11) : (v == 13 ? t13 : t15);
     if (started) {
       for (int k = 0; k < L; ++k) r = fp_sqr(r);
-      r = fp_mul(r, t);
+      r = fp_mul(r, tv);
     } else {
-      r = t;
+      r = tv;
       started = true;
     }
     i -= L;
@@ -468,7 +480,7 @@ TBG_NI Fp fp_pow_const(const Fp& a, const uint32_t (&w)[NW]) {
 
 // Fermat: a^(p-2), ~380 squarings + ~95 products in one dependent chain
 // (0.44 ms on a lone lane, profiles/r03/wide_fe.txt).
-TBG_HD Fp fp_inv_fermat(const Fp& a) { return fp_pow_const<EXP_INV_BITS>(a, EXP_INV_WORDS); }
+TBG_HD Fp fp_inv_fermat(const Fp& a) { return fp_pow_const<EXP_INV_BITS, EXP_INV_WORDS>(a); }
 
 // ---- plain-integer limb helpers for the binary inversion (values < 2^392,
 // limbs normalised to 28 bits)

@@ -354,7 +354,7 @@ TBG_NI G2J iso3_to_jac(const Fp2& x, const Fp2& y) {
 TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) {
   Fp2 a = fp2_reduce(a_in);
   Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
-  Fp gamma = fp_pow_const<EXP_SQRT_BITS>(norm, EXP_SQRT_WORDS);
+  Fp gamma = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS, 4>(norm);
   sq = fp_eq(fp_sqr(gamma), norm);
   if (!sq) {
     // gamma^2 = -norm(a); K gamma is a root of norm(Z) norm(a) = norm(Z a)
@@ -364,7 +364,7 @@ TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) {
   if (fp_is_zero(a.c1)) return false;
   Fp inv2 = fp_from_const(INV2_M);
   Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);
-  Fp t = fp_pow_const<EXP_PM3D4_BITS>(delta, EXP_PM3D4_WORDS);  // delta^((p-3)/4)
+  Fp t = fp_pow_const<EXP_PM3D4_BITS, EXP_PM3D4_WORDS, 4>(delta);  // delta^((p-3)/4)
   Fp x0 = fp_mul(delta, t);
   Fp h = fp_mul(fp_mul(a.c1, t), inv2);
   bool res = fp_eq(fp_sqr(x0), delta);

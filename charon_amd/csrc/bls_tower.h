@@ -75,19 +75,19 @@ TBG_NI bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
   bool a1_zero = fp_is_zero(a.c1);
   if (a1_zero) {
     // a in Fp: sqrt(a0) or u * sqrt(-a0)
-    Fp s = fp_pow_const<EXP_SQRT_BITS>(a.c0, EXP_SQRT_WORDS);
+    Fp s = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS>(a.c0);
     if (fp_eq(fp_sqr(s), a.c0)) { out = {s, fp_zero()}; return true; }
     Fp na = fp_neg(a.c0);
-    Fp s2 = fp_pow_const<EXP_SQRT_BITS>(na, EXP_SQRT_WORDS);
+    Fp s2 = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS>(na);
     if (fp_eq(fp_sqr(s2), na)) { out = {fp_zero(), s2}; return true; }
     return false;
   }
   Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
-  Fp gamma = fp_pow_const<EXP_SQRT_BITS>(norm, EXP_SQRT_WORDS);
+  Fp gamma = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS>(norm);
   if (!fp_eq(fp_sqr(gamma), norm)) return false;
   Fp inv2 = fp_from_const(INV2_M);
   Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);  // non-zero because a1 != 0
-  Fp t = fp_pow_const<EXP_PM3D4_BITS>(delta, EXP_PM3D4_WORDS);  // delta^((p-3)/4)
+  Fp t = fp_pow_const<EXP_PM3D4_BITS, EXP_PM3D4_WORDS>(delta);  // delta^((p-3)/4)
   Fp x0 = fp_mul(delta, t);
   Fp x0sq = fp_sqr(x0);
   Fp2 r;
@@ -109,7 +109,7 @@ TBG_NI bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
 TBG_NI bool fp2_is_square(const Fp2& a) {
   Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
   if (fp_is_zero(norm)) return true;
-  Fp l = fp_pow_const<EXP_LEGENDRE_BITS>(norm, EXP_LEGENDRE_WORDS);
+  Fp l = fp_pow_const<EXP_LEGENDRE_BITS, EXP_LEGENDRE_WORDS>(norm);
   return fp_eq(l, fp_one());
 }
 
