@@ -398,6 +398,8 @@ def main():
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
+    ap.add_argument("--subgroup-batch", type=int, default=0,
+                    help="tbg_config.subgroup_batch: 0 auto (batched G2 subgroup test while clean), 1 on, 2 off")
     ap.add_argument("--gident", type=int, default=0,
                     help="level 1g (tbg_config.gident): 0 off, 1 unresolved groups to level 3, 2 to level 1.5")
     ap.add_argument("--inject", type=float, default=None,
@@ -450,7 +452,8 @@ def main():
     # only the first `inflight` slots)
     e = eng.Engine(device, slots=max(args.inflight, 1) + (1 if args.api_batches else 0),
                    verify_mode=args.verify_mode, rlc_group=args.rlc_group,
-                   rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot, gident=args.gident)
+                   rlc_chunk=args.rlc_chunk, streams_per_slot=args.streams_per_slot, gident=args.gident,
+                   subgroup_batch=args.subgroup_batch)
     # `inflight` engine slots each hold `merge` independent caller batches
     # submitted together (tbg_submit_group: one device batch, one launch per
     # kernel for all of them) and stay resident; the timed region replays the
@@ -552,7 +555,7 @@ def main():
         "config": {"workload": WORKLOADS[args.workload].format(dvs=args.dvs, inject=args.inject),
                    "partials_per_step_per_gpu": int(len(b.identifiers)), "parallelism": f"shard{ws}",
                    "inflight_launches": args.inflight, "batches_per_launch": M,
-                   "rlc_group": group_used, "gident": args.gident,
+                   "rlc_group": group_used, "gident": args.gident, "subgroup_batch": args.subgroup_batch,
                    "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         "fallback_levels": fallback,

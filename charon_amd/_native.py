@@ -183,6 +183,7 @@ class TbgConfig(ctypes.Structure):
         ("rlc_batch", ctypes.c_uint32),
         ("gident", ctypes.c_uint32),
         ("fb_window", ctypes.c_uint32),
+        ("subgroup_batch", ctypes.c_uint32),
     ]
 
 
@@ -207,6 +208,7 @@ SIGNATURES = {
     "tbg_fetch_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "tbg_fetch_level0": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "tbg_fetch_fallback": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "tbg_fetch_subgroup": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "tbg_slot_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_last_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "tbg_sk_to_pk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),

@@ -42,6 +42,34 @@ TBG_HD uint64_t rlc_scalar(const uint32_t (&seed)[8], uint32_t i) {
   return r ? r : 1;
 }
 
+// The batched subgroup test's coefficients of partial i (k_sgb.hip): 18
+// signed digits c_k in [-6, 6] -- uniform mod 13 -- from the same keyed
+// compression function on a separate message (a tag byte after i), four
+// base-13 digits per 32-bit word (13^4 = 28561: bias < 2^-17 per digit).
+TBG_HD void sgb_digits(const uint32_t (&seed)[8], uint32_t i, int32_t (&c)[18]) {
+  uint8_t blk[64];
+  for (int k = 0; k < 8; ++k) {
+    blk[4 * k] = (uint8_t)(seed[k] >> 24);
+    blk[4 * k + 1] = (uint8_t)(seed[k] >> 16);
+    blk[4 * k + 2] = (uint8_t)(seed[k] >> 8);
+    blk[4 * k + 3] = (uint8_t)seed[k];
+  }
+  for (int k = 32; k < 64; ++k) blk[k] = 0;
+  blk[32] = (uint8_t)(i >> 24);
+  blk[33] = (uint8_t)(i >> 16);
+  blk[34] = (uint8_t)(i >> 8);
+  blk[35] = (uint8_t)i;
+  blk[36] = 0x53;  // 'S': not rlc_scalar's message
+  blk[37] = 0x80;
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au, 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  sha256_block(h, blk);
+  for (int k = 0; k < 18; ++k) {
+    uint32_t w = h[k >> 2] % 28561u;
+    for (int j = 0; j < (k & 3); ++j) w /= 13u;
+    c[k] = (int32_t)(w % 13u) - 6;
+  }
+}
+
 TBG_HD void rlc_digits(uint64_t r, uint32_t (&u)[4]) {
   for (int k = 0; k < 4; ++k) u[k] = (uint32_t)((r >> (16 * k)) & 0xFFFF);
 }

@@ -95,6 +95,7 @@ struct Slot {
   hipEvent_t done = nullptr;
   float ms[8] = {};
   uint64_t seen_bad = 0, seen_total = 0;  // invalid / verified partials of the parts collected so far
+  uint64_t seen_nsub = 0, seen_dec = 0;   // non-subgroup / all partials of the parts collected so far
   tbg::DevBatch B{};           // device view of the last batch (resident until the slot is reused)
   size_t w_out = 0;
 };
@@ -127,6 +128,8 @@ struct tbg_ctx {
   uint64_t seed_ctr = 0;
   uint32_t gident = TBG_GIDENT_OFF;  // level 1g routing (tbg_config.gident)
   uint32_t fb_window = TBG_FB_WINDOW;  // fallback line buffer positions per pass (tbg_config.fb_window)
+  uint32_t sgb_mode = TBG_SGB_AUTO;    // batched subgroup test (tbg_config.subgroup_batch)
+  double nonsub_ema = 0.0;  // exponential average of the non-subgroup share of collected partials
 };
 
 #define HIP_TRY(x)                       \
@@ -210,6 +213,8 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   if (cfg && cfg->gident > TBG_GIDENT_CHUNKS) { delete c; return TBG_E_INVALID_ARG; }
   c->gident = cfg ? cfg->gident : (uint32_t)TBG_GIDENT_OFF;
   if (cfg && cfg->fb_window) c->fb_window = cfg->fb_window;
+  if (cfg && cfg->subgroup_batch > TBG_SGB_OFF) { delete c; return TBG_E_INVALID_ARG; }
+  if (cfg) c->sgb_mode = cfg->subgroup_batch;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->retire_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->keys_ready, hipEventDisableTiming) != hipSuccess) {
@@ -595,6 +600,16 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_blines = sec(l0 ? 4ull * LINES_WORDS : 0);
   size_t w_bf = sec(l0 ? 4ull * 3 * 4 * NL : 0);
   size_t w_gf = sec(l0 ? 4ull * 3 * 4 * NL * grp_f_entries(ng) : 0);
+  // Batched subgroup test while the collected batches carry (almost) no
+  // non-subgroup signature: groups of 512 partials, a failed group's members
+  // tested alone (k_sgb.hip); small batches test every signature alone.
+  const bool sgb = np >= SGB_MIN_PARTIALS &&
+                   (c->sgb_mode == TBG_SGB_ON || (c->sgb_mode == TBG_SGB_AUTO && c->nonsub_ema < TBG_SGB_AUTO_MAX));
+  const size_t n_sg = sgb ? sgb_groups(np) : 0;
+  size_t w_sgoff = sec(4ull * (SGB_BUCKETS + 1) * n_sg);
+  size_t w_sgent = sec(4ull * SGB_M * SGB_K * n_sg);
+  size_t w_sgpart = sec(sizeof(G2J) * SGB_BUCKETS * SGB_SPLIT * n_sg);
+  size_t w_sgbad = sec(4ull * n_sg);
   size_t w_aacc = sec(op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
   size_t w_alist = sec(op != TBG_OP_VERIFY ? 4ull * nd : 0);
   size_t w_out = o;  // outputs are contiguous so one D2H copy brings them back
@@ -781,6 +796,11 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.batch_lines = (uint32_t*)(dw + w_blines);
   B.batch_f = (uint32_t*)(dw + w_bf);
   B.grp_f = (uint32_t*)(dw + w_gf);
+  B.sgb = sgb ? 1u : 0u;
+  B.sgb_off = (uint32_t*)(dw + w_sgoff);
+  B.sgb_ent = (uint32_t*)(dw + w_sgent);
+  B.sgb_part = (G2J*)(dw + w_sgpart);
+  B.sgb_bad = (uint32_t*)(dw + w_sgbad);
   B.agg_acc = (G2J*)(dw + w_aacc);
   B.agg_list = (uint32_t*)(dw + w_alist);
 
@@ -803,6 +823,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   }
   s->parts = std::move(parts);
   s->seen_bad = s->seen_total = 0;
+  s->seen_nsub = s->seen_dec = 0;
   s->busy = true;
   s->ticket = s->parts[0].ticket;
   s->op = op;
@@ -878,6 +899,13 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     s->seen_bad += bad;
     s->seen_total += q->np;
   }
+  if (q->np) {  // the batched subgroup test's input: non-subgroup share of all partials
+    const int32_t* st = (const int32_t*)s->h_out;
+    uint32_t ns = 0;
+    for (uint32_t i = 0; i < q->np; ++i) ns += st[q->p0 + i] == TBG_PS_ERR_SUBGROUP ? 1u : 0u;
+    s->seen_nsub += ns;
+    s->seen_dec += q->np;
+  }
   chain_times(s->ev, s->ms);
   memcpy(c->last_ms, s->ms, sizeof(c->last_ms));
   part_done(s, q);
@@ -886,6 +914,10 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
   if (!s->busy && s->seen_total) {
     c->invalid_ema = 0.5 * c->invalid_ema + 0.5 * (double)s->seen_bad / (double)s->seen_total;
     s->seen_bad = s->seen_total = 0;
+  }
+  if (!s->busy && s->seen_dec) {
+    c->nonsub_ema = 0.5 * c->nonsub_ema + 0.5 * (double)s->seen_nsub / (double)s->seen_dec;
+    s->seen_nsub = s->seen_dec = 0;
   }
   return TBG_OK;
 }
@@ -1055,6 +1087,23 @@ int tbg_fetch_fallback(tbg_ctx* c, tbg_ticket t, uint32_t* out8) {
   out8[7] = s->op == TBG_OP_AGGREGATE || !s->B.rlc_batch ? (uint32_t)TBG_L0_NOT_RUN
             : cnt[CNT_L0_OK]                              ? (uint32_t)TBG_L0_PASSED
                                                           : (uint32_t)TBG_L0_FAILED;
+  return TBG_OK;
+}
+
+int tbg_fetch_subgroup(tbg_ctx* c, tbg_ticket t, uint32_t* out2) {
+  if (!c || !out2) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = find_ticket(c, t, false, nullptr);
+  if (!s) return TBG_E_TICKET;
+  HIP_TRY(hipSetDevice(c->device));
+  out2[0] = out2[1] = 0;
+  if (!s->B.sgb) return TBG_OK;
+  const uint32_t n_sg = sgb_groups(s->n_partials);
+  std::vector<uint32_t> bad(n_sg);
+  HIP_TRY(hipMemcpyAsync(bad.data(), s->B.sgb_bad, 4ull * n_sg, hipMemcpyDeviceToHost, s->st));
+  HIP_TRY(hipStreamSynchronize(s->st));
+  out2[0] = n_sg;
+  for (uint32_t g = 0; g < n_sg; ++g) out2[1] += bad[g] ? 1u : 0u;
   return TBG_OK;
 }
 

@@ -129,6 +129,15 @@ struct DevBatch {
   uint32_t* batch_lines;  // [LINES_WORDS] Miller lines of S (-g1 folded in)
   uint32_t* batch_f;      // [3][4 NL] Miller product of the S pair (quad layout)
   uint32_t* grp_f;        // [GRP_F_ENTRIES(n_groups)][3][4 NL] each group's P-chunk product, then the product tree
+  // batched subgroup test of the decoded signatures (k_sgb.hip): per group
+  // of SGB_M consecutive partials, SGB_K random combinations sum c_i s_i with
+  // c_i uniform mod 13 are tested psi(Q) == [x] Q; only the members of a
+  // failed group take the per-signature test (k_subgroup_sigs)
+  uint32_t sgb;           // 1: the batched test runs (0: every signature is tested alone)
+  uint32_t* sgb_off;      // [n_sg][SGB_BUCKETS + 1] bucket offsets into the group's entries
+  uint32_t* sgb_ent;      // [n_sg][SGB_M * SGB_K] entries: member << 1 | negative
+  G2J* sgb_part;          // [n_sg][SGB_BUCKETS][SGB_SPLIT] bucket slice sums
+  uint32_t* sgb_bad;      // [n_sg] 1: some combination is outside G2 (members tested alone)
   // recombination (k_aggregate.hip)
   G2J* agg_acc;           // [n_duties] integer-coefficient sums awaiting [1/D] (listed duties only)
   uint32_t* agg_list;     // [n_duties] duties whose Lagrange denominator D > 1
@@ -152,6 +161,18 @@ enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS =
 constexpr uint32_t MSM_BUCKETS = 32768;
 constexpr uint32_t MSM_SPLIT = 4;  // slices per bucket (k_msm_bucket_part)
 constexpr uint32_t MSM_SUM_ENTRIES = 128;
+// Batched subgroup test (k_sgb.hip).  A point of E2(Fp2) outside G2 has a
+// component of order divisible by a prime factor of the G2 cofactor, the
+// smallest of which is 13: with c_i uniform mod 13 (signed digits -6..6) a
+// combination hides such a component with probability <= 1/13, so SGB_K =
+// 18 independent combinations leave 13^-18 < 2^-66.
+constexpr uint32_t SGB_M = 512;      // consecutive partials per group
+constexpr uint32_t SGB_K = 18;       // combinations per group
+constexpr uint32_t SGB_V = 6;        // buckets per combination (|c| = 1..6)
+constexpr uint32_t SGB_BUCKETS = SGB_K * SGB_V;
+constexpr uint32_t SGB_SPLIT = 4;    // slices per bucket (~20 additions each at SGB_M = 512)
+constexpr uint32_t SGB_MIN_PARTIALS = 2 * SGB_M;  // smaller batches test each signature alone
+TBG_HD inline uint32_t sgb_groups(uint32_t n_partials) { return (n_partials + SGB_M - 1) / SGB_M; }
 // Level-0 product tree over the groups' P-chunk products.  Each pass is a
 // chain of F - 1 Fp12 products on one lane group (~24 us each at one wave per
 // SIMD), so the tree's latency ~ log_F(n) * F is smallest near F = 4 (16: 1.3
@@ -220,6 +241,8 @@ void launch_sum_g2(const uint8_t* sigs96, const SumPlan& p, uint8_t* out96, int3
                    hipStream_t st);
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st);
 void launch_decode_sigs(const DevBatch& B, hipStream_t st);
+// the batched subgroup test (B.sgb): sort, bucket sums, combination checks
+void launch_subgroup_batch(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);
 void launch_hash_clear(const DevBatch& B, hipStream_t st);
 void launch_h_lines(const DevBatch& B, hipStream_t st);

@@ -27,6 +27,7 @@ TIMING_KEYS = ["decode", "hash", "combine", "h_lines", "verify", "lagrange", "ag
 VERIFY_RLC, VERIFY_EACH = 0, 1
 RLC_L0_AUTO, RLC_L0_ON, RLC_L0_OFF = 0, 1, 2   # tbg_config.rlc_batch
 GIDENT_OFF, GIDENT_L3, GIDENT_CHUNKS = 0, 1, 2  # tbg_config.gident
+SGB_AUTO, SGB_ON, SGB_OFF = 0, 1, 2           # tbg_config.subgroup_batch
 L0_NOT_RUN, L0_PASSED, L0_FAILED = 0, 1, 2     # tbg_fetch_level0
 E_PENDING = -6
 
@@ -73,12 +74,12 @@ class Engine:
 
     def __init__(self, device: int = 0, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0,
                  rlc_seed: int = 0, rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0,
-                 gident: int = GIDENT_OFF, fb_window: int = 0):
+                 gident: int = GIDENT_OFF, fb_window: int = 0, subgroup_batch: int = SGB_AUTO):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
                                 rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch,
-                                gident=gident, fb_window=fb_window)
+                                gident=gident, fb_window=fb_window, subgroup_batch=subgroup_batch)
         h = ctypes.c_void_p()
         rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
         self._check(rc, "tbg_init")
@@ -232,6 +233,14 @@ class Engine:
         return dict(zip(["groups", "group_searches", "chunks", "chunk_searches", "duty_searches", "partial_checks",
                          "group_size", "level0"], out.tolist()))
 
+    def subgroup(self, ticket) -> dict:
+        """Batched subgroup test of the batch's last run (tbg_fetch_subgroup):
+        groups of 512 partials tested by random combinations (0: every
+        signature tested alone) and how many failed."""
+        out = np.zeros(2, dtype=np.uint32)
+        self._check(self._lib.tbg_fetch_subgroup(self._h, ticket, _ptr(out)), "tbg_fetch_subgroup")
+        return dict(zip(["groups", "failed"], out.tolist()))
+
     def slot_bytes(self, ticket) -> tuple:
         """(device bytes, pinned host bytes) of the slot holding the ticket's batch."""
         dev, pin = ctypes.c_uint64(), ctypes.c_uint64()
@@ -309,12 +318,12 @@ class MultiEngine:
 
     def __init__(self, devices, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0, rlc_seed: int = 0,
                  rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0, gident: int = GIDENT_OFF,
-                 fb_window: int = 0):
+                 fb_window: int = 0, subgroup_batch: int = SGB_AUTO):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=0, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
                                 rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch,
-                                gident=gident, fb_window=fb_window)
+                                gident=gident, fb_window=fb_window, subgroup_batch=subgroup_batch)
         devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
         h = ctypes.c_void_p()
         rc = self._lib.tbg_multi_init(ctypes.byref(cfg), _ptr(devs), len(devs), ctypes.byref(h))
@@ -324,6 +333,8 @@ class MultiEngine:
         self.devices = devs.tolist()
         self.uid = next(_serial)
         self._keep = {}
+        import weakref
+        self._borrowed = weakref.WeakSet()  # per-context Engines handed out by context()
 
     _check = Engine._check
     _batch = Engine._batch
@@ -334,6 +345,11 @@ class MultiEngine:
 
     def close(self):
         if getattr(self, "_h", None):
+            # the borrowed per-context Engines lose their handles first: a
+            # later call through one raises EngineError (a NULL context)
+            # instead of reaching freed native memory
+            for e in list(getattr(self, "_borrowed", ())):
+                e._h = None
             self._lib.tbg_multi_destroy(self._h)
             self._h = None
 
@@ -350,7 +366,9 @@ class MultiEngine:
         h = self._lib.tbg_multi_context(self._h, i)
         if not h:
             raise EngineError(f"tbg_multi_context: no context {i}")
-        return _BorrowedEngine(self._lib, h, self.devices[i])
+        e = _BorrowedEngine(self._lib, h, self.devices[i], self)
+        self._borrowed.add(e)
+        return e
 
     def load_pubkeys(self, pk48) -> tuple[int, np.ndarray]:
         a = _u8(pk48, 48)
@@ -403,8 +421,9 @@ class MultiEngine:
 class _BorrowedEngine(Engine):
     """An Engine over a context owned by a MultiEngine (tbg_multi_context)."""
 
-    def __init__(self, lib, handle, device):
+    def __init__(self, lib, handle, device, parent):
         self._lib = lib
+        self._parent = parent  # keeps the owning MultiEngine (and its contexts) alive
         self._h = ctypes.c_void_p(handle)
         self.device = device
         self.uid = next(_serial)

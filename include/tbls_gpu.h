@@ -104,7 +104,20 @@ typedef struct {
   uint32_t fb_window;     /* list positions per pass of the fallback levels' shared
                            * Miller-line buffer (22.8 KB of HBM each; 0 -> 32768):
                            * longer lists run in several passes                       */
+  uint32_t subgroup_batch; /* G2 subgroup checks of the decoded signatures:
+                           * TBG_SGB_AUTO (0) random-combination tests per group of
+                           * 512 partials, each member tested alone only when its
+                           * group fails, while the non-subgroup share average is
+                           * below TBG_SGB_AUTO_MAX; TBG_SGB_ON always; TBG_SGB_OFF
+                           * every signature alone.  Batches below 1024 partials
+                           * always test each signature alone.                        */
 } tbg_config;
+#define TBG_SGB_AUTO 0
+#define TBG_SGB_ON 1
+#define TBG_SGB_OFF 2
+/* (with 512 partials per group ~10 % of the groups fail at this share: the
+ * batched test then costs ~0.6 of testing every signature alone) */
+#define TBG_SGB_AUTO_MAX 2e-4
 #define TBG_GIDENT_OFF 0
 #define TBG_GIDENT_L3 1
 #define TBG_GIDENT_CHUNKS 2
@@ -235,6 +248,11 @@ int tbg_fetch_level0(tbg_ctx* ctx, tbg_ticket ticket, int32_t* state);
  * duties searched at level 2b, partials checked one by one at level 3,
  * duties per group, level 0 (TBG_L0_*)]. */
 int tbg_fetch_fallback(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out8);
+/* Batched subgroup test of a collected batch's last run (tbg_config.
+ * subgroup_batch): out2 = [groups of 512 partials tested by random
+ * combinations (0: every signature was tested alone), groups that failed
+ * (their members were then tested one by one)]. */
+int tbg_fetch_subgroup(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out2);
 /* Footprint of the slot holding the ticket's batch: device bytes (input
  * arena + work arena) and pinned host bytes (staging both ways). */
 int tbg_slot_bytes(tbg_ctx* ctx, tbg_ticket ticket, uint64_t* device_bytes, uint64_t* pinned_bytes);
