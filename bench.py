@@ -53,6 +53,10 @@ METRIC = "verified+aggregated 3-of-4 threshold BLS sigs/sec at 1/2/4/8 MI355X"
 # 1 / 2 / 4 / 8 waves per SIMD); the 4-cycle issue model gives 39.3 T at
 # 2.4 GHz (256 CU x 4 SIMD x 32 lanes / 2).  See DESIGN.md.
 PEAK_MAD_TOPS = 32.8
+# The clock-derived ceiling of a half-rate 64-bit multiply-add: 256 CU x 4
+# SIMD x 16 lanes per cycle x 2.4 GHz (MI355X_MICROARCH.md gives no integer
+# multiply peak); the measured 32.8 T is 83 % of it.  Both fractions are printed.
+PEAK_MAD_TOPS_CLOCK = 39.3
 
 
 def dist_setup():
@@ -114,7 +118,7 @@ def work_model():
 
 # Stages of the kernel chain (tbg_last_timings order) and their kernels.
 STAGE_KERNELS = {
-    "decode": ["k_decode_sigs", "k_subgroup_sigs"],
+    "decode": ["k_decode_sigs", "k_sgb_sort", "k_sgb_bucket", "k_sgb_combine", "k_sgb_test", "k_subgroup_sigs"],
     "hash": ["k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
     "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_bucket_part", "k_msm_tree", "k_msm_tree_final", "k_msm_scan", "k_msm_scatter",
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
@@ -200,6 +204,9 @@ def kernel_roofline(wm, kp, items, tm, batches):
             "achieved": round(ach, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
             "frac": round(ach / PEAK_MAD_TOPS, 4),
             "frac_fp300": round(fp_mul_per_s * SURVEY_MADS_PER_FP_MUL / 1e12 / PEAK_MAD_TOPS, 4),
+            "peak_clock_derived": PEAK_MAD_TOPS_CLOCK,
+            "frac_clock_derived": round(ach / PEAK_MAD_TOPS_CLOCK, 4),
+            "frac_fp300_clock_derived": round(fp_mul_per_s * SURVEY_MADS_PER_FP_MUL / 1e12 / PEAK_MAD_TOPS_CLOCK, 4),
             "fp_mul_per_s": round(fp_mul_per_s, 1),
             "traffic": traffic, "traffic_unit": "bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
                                                 "profiles/traffic_latest.json)" if traffic is not None else None,
@@ -212,15 +219,18 @@ def kernel_roofline(wm, kp, items, tm, batches):
                         "command: tools/roofline_from_trace.py"}
 
 
-def pipeline_roofline(wm, value, l0, t, n):
+def pipeline_roofline(wm, value, l0, t, n, sgb=True):
     """roofline_pipeline: the whole chain, work model x rate (config 2 shape)."""
     if not wm or (t, n) != (3, 4):
         return None
     unit = wm["mads"]["unit_3of4_l0" if l0 else "unit_3of4_rlc"]
+    if not sgb:  # every signature's subgroup test alone
+        unit += 4 * (wm["mads"]["decode_sig"] - wm["mads"]["decode_sig_batched_subgroup"])
     ach = value * unit / 1e12
     return {"bound": "valu-int-mul", "kernel": "the whole kernel chain (launches in flight together)",
             "achieved": round(ach, 3), "peak": PEAK_MAD_TOPS, "unit": "T u32-mad/s",
-            "frac": round(ach / PEAK_MAD_TOPS, 4), "work_per_unit_mads": unit,
+            "frac": round(ach / PEAK_MAD_TOPS, 4), "frac_clock_derived": round(ach / PEAK_MAD_TOPS_CLOCK, 4),
+            "work_per_unit_mads": unit,
             "schedule": "level 0 (batch-wide check, bucket MSM)" if l0 else "level-1 groups",
             "reference_schedule_mads_per_unit": wm["mads"]["unit_3of4_single_lane_schedule"],
             "reference_schedule_equivalent_tmads": round(value * wm["mads"]["unit_3of4_single_lane_schedule"] / 1e12,
@@ -293,6 +303,61 @@ def api_pipeline(e, eng, batches, inflight, n_batches, merge):
             "path": "tbg_submit_group + tbg_collect (pinned staging, H2D, chain, D2H); results checked after the clock"}
 
 
+def latency_probe(e_load, eng, load_plan, sizes=(1, 64, 1024, 10000), reps=(30, 30, 12, 6)):
+    """Submit -> collect latency of small batches (the reference verifies a
+    peer's set inside a 5 s handler context, core/parsigex/parsigex.go:70-71,
+    and the local VC's submission synchronously, core/validatorapi/
+    validatorapi.go:228-287; tbls.Verify of one partial is a one-duty batch):
+    p50 / p99 over `reps` tbg_submit + tbg_collect of each size on an idle
+    context, then again on a second context while the first replays the
+    headline launches (`load_plan`) in a background thread.  Every result is
+    checked; the first call of each size (arena allocation) is not counted."""
+    import threading
+    from tools.workload import make_batch
+    e = eng.Engine(e_load.device, slots=2)
+    try:
+        bs = {n: make_batch(e, n, 3, 4, seed=7000 + n) for n in sizes}
+
+        def one(b):
+            t0 = time.perf_counter()
+            r = e.run(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
+                      duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+            dt = (time.perf_counter() - t0) * 1e3
+            if not batch_exact(r, b, eng):
+                raise RuntimeError("latency probe: result differs")
+            return dt
+
+        def series():
+            out = {}
+            for n, k in zip(sizes, reps):
+                one(bs[n])
+                t = np.array([one(bs[n]) for _ in range(k)])
+                out[str(n)] = {"p50_ms": round(float(np.percentile(t, 50)), 3),
+                               "p99_ms": round(float(np.percentile(t, 99)), 3), "samples": k}
+            return out
+
+        idle = series()
+        stop = threading.Event()
+
+        def load():
+            while not stop.is_set():
+                e_load.replay_plan(*load_plan)
+
+        th = threading.Thread(target=load, daemon=True)
+        th.start()
+        try:
+            time.sleep(0.2)
+            loaded = series()
+        finally:
+            stop.set()
+            th.join()
+        return {"idle": idle, "under_headline_load": loaded,
+                "path": "tbg_submit + tbg_collect of one VERIFY_AGGREGATE batch (3-of-4) on its own context; "
+                        "load = the headline launches replayed on another context of the same GPU"}
+    finally:
+        e.close()
+
+
 def batch_exact(res, b, eng):
     """Every partial verifies iff it was not injected, every duty with t
     valid partials aggregates to the group signature, the others fail."""
@@ -302,6 +367,27 @@ def batch_exact(res, b, eng):
     if not np.array_equal(ok, b.expect_ok):
         return False
     return bool(np.array_equal(res.agg[ok], b.group_sig[ok]))
+
+
+def host_side(hs, duties, wall_s):
+    """The host share of the multi-context product path, timed inside the
+    library (tbg_multi_host_stats): CPU time of the sub-batch builds, the
+    packing into pinned staging and the gather (copy-out + counts), and the
+    DV-duty rate those would sustain spread over the box's 16 cores -- host
+    side only, no scaling curve (the GPUs are not involved in the figure)."""
+    ms = lambda ns: round(ns / 1e6, 3)  # noqa: E731
+    cpu_ns = hs["build_ns"] + hs["ctx_pack_ns"] + hs["ctx_gather_ns"]
+    return {
+        "label": "host side only, no scaling curve",
+        "duties": duties, "wall_ms": round(wall_s * 1e3, 3),
+        "submit_wall_ms": ms(hs["submit_wall_ns"]), "collect_wall_ms": ms(hs["collect_wall_ns"]),
+        "build_cpu_ms": ms(hs["build_ns"]), "pack_cpu_ms": ms(hs["ctx_pack_ns"]),
+        "enqueue_cpu_ms": ms(hs["ctx_enqueue_ns"]), "gather_cpu_ms": ms(hs["ctx_gather_ns"]),
+        "device_wait_ms": ms(hs["ctx_wait_ns"]),
+        "dv_duties_per_host_cpu_s": round(duties / (cpu_ns / 1e9), 1) if cpu_ns else None,
+        "dv_duties_per_s_on_16_cores": round(16 * duties / (cpu_ns / 1e9), 1) if cpu_ns else None,
+        "workers": "persistent per-context host workers (tbls_multi.hip Pool); pack / gather per context",
+    }
 
 
 def config4_multi(args):
@@ -342,10 +428,12 @@ def config4_multi(args):
 
         res = one_round()  # untimed: the first round allocates every context's arenas
         rounds = max(1, args.steps)
+        m.host_stats(reset=True)
         t0 = time.perf_counter()
         for _ in range(rounds):
             res = one_round()
         dt = time.perf_counter() - t0
+        hs = m.host_stats()
         ps = np.concatenate([r.partial_status for r in res])
         ds = np.concatenate([r.duty_status for r in res])
         agg = np.concatenate([r.agg for r in res])
@@ -362,7 +450,8 @@ def config4_multi(args):
                            "contexts": len(devs), "caller_batches": K,
                            "path": "tbg_multi_submit_group + tbg_multi_collect (host packing, PCIe, chains, "
                                    "gather); one step = the whole batch"},
-                "exact": exact, "generation_s": round(gen_s, 1)}
+                "exact": exact, "generation_s": round(gen_s, 1),
+                "host_side": host_side(hs, args.dvs * rounds, dt)}
     finally:
         m.close()
 
@@ -398,6 +487,7 @@ def main():
     ap.add_argument("--rlc-group", type=int, default=0, help="duties per RLC group (0 = engine default)")
     ap.add_argument("--rlc-chunk", type=int, default=0, help="duties per Miller quad (0 = engine default)")
     ap.add_argument("--streams-per-slot", type=int, default=0, help="1 (default) or 2")
+    ap.add_argument("--latency", type=int, default=1, help="1: the small-batch latency side key (latency_probe)")
     ap.add_argument("--subgroup-batch", type=int, default=0,
                     help="tbg_config.subgroup_batch: 0 auto (batched G2 subgroup test while clean), 1 on, 2 off")
     ap.add_argument("--gident", type=int, default=0,
@@ -527,6 +617,7 @@ def main():
     l0_state = e.level0(tickets[0])
     fallback = e.fallback(tickets[0])  # per-level fallback work of the slot's last run
     slot_dev, slot_pinned = e.slot_bytes(tickets[0])
+    subgroup = e.subgroup(tickets[0])  # batched subgroup test of the slot's last run
 
     units = args.dvs * args.steps * ws
     value = units / elapsed
@@ -541,8 +632,11 @@ def main():
     wm = work_model()
     roofline = kernel_roofline(wm, kp, launch_items(batches[0], group_used or 16), traffic_model(), M)
     # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
-    roofline_pipeline = pipeline_roofline(wm, value / ws, l0_state == eng.L0_PASSED, args.t, args.n) \
+    roofline_pipeline = pipeline_roofline(wm, value / ws, l0_state == eng.L0_PASSED, args.t, args.n,
+                                          subgroup["groups"] > 0) \
         if args.workload in ("config2", "config4") else None
+    # (before api_pipeline: the load replays the resident launches)
+    lat = latency_probe(e, eng, plan(3 * M)) if args.latency and rank == 0 and args.workload == "config2" else None
     # (reuses the engine's slots: after the replays and the isolated pass)
     api = api_pipeline(e, eng, flat, args.inflight + 1, args.api_batches, M) if args.api_batches else None
 
@@ -559,10 +653,12 @@ def main():
                    "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         "fallback_levels": fallback,
+        "subgroup_batch": subgroup,
         "slot_bytes": {"device": int(slot_dev), "pinned_host": int(slot_pinned), "batches_per_slot": M},
         "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kernel_ms.items()},
         "pcie_inclusive_ms_first_batch": round(pcie_ms, 3),
         "api_pipeline": api,
+        "small_batch_latency": lat,
         "isolated_batch_ms": iso,
         "isolated_kernel_ms": {k: round(v[0], 4) for k, v in sorted(kp.items(), key=lambda kv: -kv[1][0])
                                if v[0] >= 0.05},

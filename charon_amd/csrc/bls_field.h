@@ -684,17 +684,23 @@ TBG_HD Fp fp_inv_bgcd(const Fp& a) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) pinv *= 2 - (uint64_t)P.v[0] * pinv;
   S62 f = P, g = s62_from_fp(x), d = {{0, 0, 0, 0, 0, 0, 0}}, e = {{1, 0, 0, 0, 0, 0, 0}};
-  int64_t delta = 1;
-  for (int it = 0; it < 40; ++it) {  // <= ~18 batches for 381-bit values
+  int64_t delta = 1, gz = 1;
+  for (int it = 0; it < 40 && gz != 0; ++it) {  // <= ~18 batches for 381-bit values
     int64_t u, v, q, r;
     delta = divsteps62(delta, (uint64_t)f.v[0], (uint64_t)g.v[0], u, v, q, r);
     s62_update(f, g, u, v, q, r, nullptr, 0);
     s62_update(d, e, u, v, q, r, &P, pinv);
-    int64_t gz = 0;
+    gz = 0;
 #pragma unroll
     for (int i = 0; i < 7; ++i) gz |= g.v[i];
-    if (gz == 0) break;
   }
+  // convergence (host bound checks): g reached 0 and f = +-1 --
+  // a change to delta, the batch width or the limb form that broke the
+  // iteration bound would otherwise return a wrong value in [0, 2p)
+  TBG_BOUND(gz == 0, "fp_inv_bgcd: g reached 0 within 40 batches");
+  TBG_BOUND((f.v[0] == 1 && (f.v[1] | f.v[2] | f.v[3] | f.v[4] | f.v[5] | f.v[6]) == 0) ||
+                ((f.v[0] & f.v[1] & f.v[2] & f.v[3] & f.v[4] & f.v[5]) == (int64_t)M62 && f.v[6] == -1),
+            "fp_inv_bgcd: f = +-1");
   // f = +-1 = d x (mod p): 1/x = sign(f) d; |d| < 41 p, shifted by 64 p into (23 p, 105 p)
   const bool neg = f.v[6] < 0;
   S62 y;

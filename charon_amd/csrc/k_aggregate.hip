@@ -7,12 +7,26 @@
 
 namespace tbg {
 
-// The speculative pass (SPEC) and the regular pass after it: see
-// participates<SPEC> (tbls_launch.h).  spec_done: a level-0 pass confirmed
-// the speculative results (the regular pass leaves them).
+// The speculative pass (SPEC: the candidates taken as valid, run as soon as
+// they are final while level 0 is on) and the regular pass after the checks,
+// which returns at once after a level-0 pass and otherwise aggregates every
+// duty again.  With TBG_SPEC_ALWAYS (tbls_launch.h; measured slower) every
+// VERIFY_AGGREGATE chain speculates and the regular pass redoes only the
+// duties whose participant set the checks changed (spec_redo): a duty none
+// of whose partials turned out INVALID keeps the speculative aggregate.
 __device__ __forceinline__ bool spec_skip(const DevBatch& B, bool spec) {
-  if (spec) return B.counters[CNT_L0_BAD] != 0;  // level 0 cannot pass: no speculation
-  return B.rlc_batch && B.op == TBG_OP_VERIFY_AGGREGATE && B.counters[CNT_L0_OK] != 0;
+  if (spec) return TBG_SPEC_ALWAYS ? false : B.counters[CNT_L0_BAD] != 0;
+  return B.op == TBG_OP_VERIFY_AGGREGATE && B.counters[CNT_L0_OK] != 0;
+}
+// (an ERR_PUBKEY mark made after the speculative pass -- the group levels'
+// k_rlc_partial2 -- changes the set too)
+__device__ __forceinline__ bool spec_redo(const DevBatch& B, uint32_t d) {
+  if (!TBG_SPEC_ALWAYS || B.op != TBG_OP_VERIFY_AGGREGATE) return true;
+  for (uint32_t j = B.duty_first[d]; j < B.duty_first[d + 1]; ++j) {
+    const int32_t st = B.partial_status[j];
+    if (st == TBG_PS_INVALID || st == TBG_PS_ERR_PUBKEY) return true;
+  }
+  return false;
 }
 
 template <bool SPEC>
@@ -21,6 +35,7 @@ __global__ void TBG_LAUNCH k_lagrange(DevBatch B) {
   if (spec_skip(B, SPEC)) return;
   if (i == 0) B.counters[CNT_AGG] = 0;  // (k_aggregate appends after this grid)
   if (i >= B.n_partials) return;
+  if (!SPEC && !spec_redo(B, B.partial_duty[i])) return;  // the speculative coefficients stand
   uint32_t* w = B.lam + 8ull * i;
   for (int j = 0; j < 8; ++j) w[j] = 0;
   if (!participates<SPEC>(B.op, B.partial_status[i])) return;
@@ -192,7 +207,9 @@ __global__ void __launch_bounds__(BINV_BLOCK, TBG_PAIR_WAVES) k_aggregate(DevBat
   if (spec_skip(B, SPEC)) return;  // (grid-uniform)
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, d = t >> 1;
   const bool lead = pair_par() == 0;
-  const bool in = d < B.n_duties;
+  // (a duty the regular pass leaves keeps the speculative output; it still
+  // takes part in the workgroup's batched inversion below)
+  const bool in = d < B.n_duties && (SPEC || spec_redo(B, d));
   uint32_t pmask = 0;
   bool fast = false;
   const int32_t st = in ? agg_status<SPEC>(B, d, lead, pmask, fast) : TBG_DS_OK;

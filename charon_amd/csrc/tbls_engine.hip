@@ -10,6 +10,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <mutex>
 #include <new>
 #include <random>
@@ -129,6 +131,10 @@ struct tbg_ctx {
   uint32_t gident = TBG_GIDENT_OFF;  // level 1g routing (tbg_config.gident)
   uint32_t fb_window = TBG_FB_WINDOW;  // fallback line buffer positions per pass (tbg_config.fb_window)
   uint32_t sgb_mode = TBG_SGB_AUTO;    // batched subgroup test (tbg_config.subgroup_batch)
+  // host-side work of the submit / collect calls (tbg_host_stats): [submits,
+  // partials submitted, pack ns, enqueue ns, collects, partials collected,
+  // gather ns, wait ns]
+  std::atomic<uint64_t> host[8] = {};
   double nonsub_ema = 0.0;  // exponential average of the non-subgroup share of collected partials
 };
 
@@ -374,9 +380,9 @@ ready:
   return rc;
 }
 
-// Level 0 on: the aggregation a level-0 pass will confirm (every candidate
-// valid), enqueued mid-chain so the launch's tail is the verification alone;
-// the regular aggregation after the checks returns at once after a pass.
+// The aggregation the checks will mostly confirm (every candidate valid),
+// enqueued mid-chain so the launch's tail is the verification plus the redo of
+// the few duties with an invalid partial (none after a level-0 pass).
 static void spec_aggregation(const DevBatch& B, hipStream_t st) {
   launch_lagrange(B, st, true);
   launch_aggregate(B, st, true);
@@ -401,7 +407,11 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
   // With one stream per slot the two independent chains run one after the
   // other, the per-message chain first (running the per-signature chain
   // first on odd slots was measured no better, round 2).
-  const bool spec = B.op == TBG_OP_VERIFY_AGGREGATE && B.rlc_batch && B.rlc_group;
+  // The aggregation runs speculatively as soon as the candidates are final
+  // (every candidate taken as valid), off the launch's serial tail, while
+  // level 0 is on (TBG_SPEC_ALWAYS: on every VERIFY_AGGREGATE chain, redoing
+  // only the duties with an invalid partial -- measured slower, round 5).
+  const bool spec = B.op == TBG_OP_VERIFY_AGGREGATE && (TBG_SPEC_ALWAYS || (B.rlc_batch && B.rlc_group));
   auto msg_chain = [&]() -> int {
     HIP_TRY(hipEventRecord(ev[3], st2));
     if (verify) launch_hash_msgs(B, st2);
@@ -629,6 +639,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   s->parts.clear();
   s->busy = true;
   lk.unlock();
+  const auto t_pack = std::chrono::steady_clock::now();
 
   // ---- pack: batch k's duties / partials / messages follow batch k-1's,
   // every index rebased by the running offsets ----
@@ -693,6 +704,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   }
   duty_first[nd] = np;
   if (verify) msg_off[nm] = MB;
+  const auto t_packed = std::chrono::steady_clock::now();
 
   lk.lock();
   // from here on a failure releases the reserved slot
@@ -815,6 +827,14 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   if (hipMemcpyAsync(s->h_out, dw + w_out, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipEventRecord(s->done, st) != hipSuccess)
     return release(TBG_E_DEVICE);
+  {
+    const auto t_end = std::chrono::steady_clock::now();
+    using ns = std::chrono::nanoseconds;
+    c->host[0] += 1;
+    c->host[1] += np;
+    c->host[2] += (uint64_t)std::chrono::duration_cast<ns>(t_packed - t_pack).count();
+    c->host[3] += (uint64_t)std::chrono::duration_cast<ns>(t_end - t_packed).count();
+  }
 
   for (uint32_t k = 0; k < n_batches; ++k) {
     parts[k].ticket = c->next_ticket++;
@@ -882,8 +902,11 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     hipEvent_t done = s->done;
     int dev = c->device;
     lk.unlock();
+    const auto t_wait = std::chrono::steady_clock::now();
     (void)hipSetDevice(dev);  // the HIP current device is per thread
     e = hipEventSynchronize(done);
+    c->host[7] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                                 t_wait).count();
     lk.lock();
     q->collecting = false;
   }
@@ -891,6 +914,7 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     part_done(s, q);
     return TBG_E_DEVICE;
   }
+  const auto t_gather = std::chrono::steady_clock::now();
   copy_part(s, *q, pst, dst, agg);
   if (s->op != TBG_OP_AGGREGATE && q->np) {  // the adaptive group size's and level 0's input
     const int32_t* st = (const int32_t*)s->h_out;  // partial statuses lead the output region
@@ -906,6 +930,10 @@ int tbg_collect(tbg_ctx* c, tbg_ticket t, int32_t* pst, int32_t* dst, uint8_t* a
     s->seen_nsub += ns;
     s->seen_dec += q->np;
   }
+  c->host[4] += 1;
+  c->host[5] += q->np;
+  c->host[6] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                               t_gather).count();
   chain_times(s->ev, s->ms);
   memcpy(c->last_ms, s->ms, sizeof(c->last_ms));
   part_done(s, q);
@@ -1104,6 +1132,12 @@ int tbg_fetch_subgroup(tbg_ctx* c, tbg_ticket t, uint32_t* out2) {
   HIP_TRY(hipStreamSynchronize(s->st));
   out2[0] = n_sg;
   for (uint32_t g = 0; g < n_sg; ++g) out2[1] += bad[g] ? 1u : 0u;
+  return TBG_OK;
+}
+
+int tbg_host_stats(tbg_ctx* c, uint64_t* out8, int reset) {
+  if (!c || !out8) return TBG_E_INVALID_ARG;
+  for (int k = 0; k < 8; ++k) out8[k] = reset ? c->host[k].exchange(0) : c->host[k].load();
   return TBG_OK;
 }
 

@@ -166,11 +166,17 @@ constexpr uint32_t MSM_SUM_ENTRIES = 128;
 // smallest of which is 13: with c_i uniform mod 13 (signed digits -6..6) a
 // combination hides such a component with probability <= 1/13, so SGB_K =
 // 18 independent combinations leave 13^-18 < 2^-66.
-constexpr uint32_t SGB_M = 512;      // consecutive partials per group
-constexpr uint32_t SGB_K = 18;       // combinations per group
-constexpr uint32_t SGB_V = 6;        // buckets per combination (|c| = 1..6)
+#ifndef TBG_SGB_M
+#define TBG_SGB_M 512
+#endif
+#ifndef TBG_SGB_SPLIT
+#define TBG_SGB_SPLIT 4
+#endif
+constexpr uint32_t SGB_M = TBG_SGB_M;  // consecutive partials per group
+constexpr uint32_t SGB_K = 18;         // combinations per group
+constexpr uint32_t SGB_V = 6;          // buckets per combination (|c| = 1..6)
 constexpr uint32_t SGB_BUCKETS = SGB_K * SGB_V;
-constexpr uint32_t SGB_SPLIT = 4;    // slices per bucket (~20 additions each at SGB_M = 512)
+constexpr uint32_t SGB_SPLIT = TBG_SGB_SPLIT;  // slices per bucket (~20 additions each at SGB_M = 512)
 constexpr uint32_t SGB_MIN_PARTIALS = 2 * SGB_M;  // smaller batches test each signature alone
 TBG_HD inline uint32_t sgb_groups(uint32_t n_partials) { return (n_partials + SGB_M - 1) / SGB_M; }
 // Level-0 product tree over the groups' P-chunk products.  Each pass is a
@@ -196,6 +202,15 @@ enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT
 TBG_HD bool fb_in_pass(const DevBatch& B, uint32_t k) { return B.fb_window == 0 || k - B.fb_base < B.fb_window; }
 TBG_HD size_t fb_slot(const DevBatch& B, uint32_t k) { return (size_t)LINES_WORDS * (k - B.fb_base); }
 
+// 1: every VERIFY_AGGREGATE chain aggregates speculatively and redoes only
+// the duties with an invalid partial; 0 (default): speculate only while level
+// 0 runs, aggregate every duty again after a failed level 0.  Measured at 1 %
+// invalid (level 0 off) and on config 5 (round 5, profiles/r05/inv1/): 1.48 /
+// 1.47 M vs 1.49 / 1.50 M and 1.17 / 1.19 M vs 1.24 / 1.24 M -- the
+// speculative pass's throughput cost outweighs the shorter redo at the tail.
+#ifndef TBG_SPEC_ALWAYS
+#define TBG_SPEC_ALWAYS 0
+#endif
 // Participation of a partial in its duty's aggregate.  SPEC: the
 // speculative aggregation that runs BEFORE verification while level 0 is on
 // (launch_chain): every candidate counts as valid, which is what a level-0
@@ -271,7 +286,7 @@ void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff
                          uint32_t n_pk, hipStream_t st);
 // spec: the speculative pass (level 0 on, before verification; skipped when
 // level 0 already cannot pass); the regular pass then returns at once if
-// level 0 passed
+// level 0 passed (TBG_SPEC_ALWAYS: see above)
 void launch_lagrange(const DevBatch& B, hipStream_t st, bool spec = false);
 void launch_aggregate(const DevBatch& B, hipStream_t st, bool spec = false);
 void launch_aggregate_finish(const DevBatch& B, hipStream_t st, bool spec = false);

@@ -8,14 +8,19 @@
 // that shares the caller's arrays by pointer offset (only duty_first is
 // rebased and the messages a range uses are re-indexed), and each context's
 // pieces are packed into ONE device batch (tbg_submit_group) and submitted
-// concurrently, one host thread per context.  Collection writes each shard's statuses and aggregates straight
+// concurrently on persistent per-context host workers.  Collection writes each shard's statuses and aggregates straight
 // into the caller's arrays at the shard's offsets, so the gather is the
 // per-DV loop order of core/parsigex/parsigex.go:101-107 and
 // core/parsigdb/memory.go:96-134 -> core/sigagg/sigagg.go:53-103 by
 // construction.  Host code only.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -116,14 +121,77 @@ int validate_split(const tbg_batch* b) {
   return TBG_OK;
 }
 
-// Run fn(i) for i in [0, n) on n threads (i = 0 on the caller's thread).
-template <class F>
-void parallel_for(uint32_t n, F fn) {
-  std::vector<std::thread> th;
-  th.reserve(n ? n - 1 : 0);
-  for (uint32_t i = 1; i < n; ++i) th.emplace_back(fn, i);
-  if (n) fn(0);
-  for (auto& t : th) t.join();
+// Persistent host workers (one per context but the first, whose piece runs
+// on the calling thread): run(n, fn) hands fn(i), i = 1 .. n - 1, to worker
+// i - 1's FIFO and waits for all of them -- no thread is created per call
+// (round 4 spawned and joined n - 1 std::threads on every submit and
+// collect).  Calls from several caller threads interleave on each worker's
+// queue.  A multi-context owns two pools, so a collect blocked on the device
+// never delays a submit queued behind it.
+class Pool {
+ public:
+  explicit Pool(uint32_t n) : q_(n) {
+    for (uint32_t w = 0; w < n; ++w) th_.emplace_back([this, w] { loop(w); });
+  }
+  ~Pool() {
+    for (auto& q : q_) {
+      std::lock_guard<std::mutex> lk(q.mu);
+      q.stop = true;
+      q.cv.notify_one();
+    }
+    for (auto& t : th_) t.join();
+  }
+  template <class F>
+  void run(uint32_t n, F fn) {
+    struct Latch {
+      std::mutex mu;
+      std::condition_variable cv;
+      uint32_t left;
+    } latch;
+    latch.left = n > 1 ? n - 1 : 0;
+    for (uint32_t i = 1; i < n; ++i) {
+      Queue& q = q_[(i - 1) % q_.size()];
+      std::lock_guard<std::mutex> lk(q.mu);
+      q.tasks.emplace_back([&fn, &latch, i] {
+        fn(i);
+        std::lock_guard<std::mutex> l2(latch.mu);
+        if (--latch.left == 0) latch.cv.notify_one();
+      });
+      q.cv.notify_one();
+    }
+    if (n) fn(0);
+    std::unique_lock<std::mutex> lk(latch.mu);
+    latch.cv.wait(lk, [&] { return latch.left == 0; });
+  }
+
+ private:
+  struct Queue {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> tasks;
+    bool stop = false;
+  };
+  void loop(uint32_t w) {
+    Queue& q = q_[w];
+    for (;;) {
+      std::function<void()> task;
+      {
+        std::unique_lock<std::mutex> lk(q.mu);
+        q.cv.wait(lk, [&] { return q.stop || !q.tasks.empty(); });
+        if (q.tasks.empty()) return;  // stopping, nothing left
+        task = std::move(q.tasks.front());
+        q.tasks.pop_front();
+      }
+      task();
+    }
+  }
+  std::vector<Queue> q_;
+  std::vector<std::thread> th_;
+};
+
+inline uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 }  // namespace
@@ -133,6 +201,12 @@ struct tbg_multi {
   std::mutex mu;
   std::unordered_map<tbg_ticket, Job> jobs;
   tbg_ticket next_ticket = 1;
+  Pool* submit_pool = nullptr;   // pieces' sub-batch builds and per-context submits
+  Pool* collect_pool = nullptr;  // shards' waits and copy-outs
+  // host-side work (tbg_multi_host_stats): [submit calls, partials, ns in
+  // sub-batch builds (summed over workers), submit wall ns, collect calls,
+  // collect wall ns]
+  std::atomic<uint64_t> host[6] = {};
 };
 
 extern "C" {
@@ -154,12 +228,21 @@ int tbg_multi_init(const tbg_config* cfg, const int32_t* devices, uint32_t n_dev
     }
     m->ctx.push_back(x);
   }
+  const uint32_t workers = n_devices > 1 ? n_devices - 1 : 1;
+  m->submit_pool = new (std::nothrow) Pool(workers);
+  m->collect_pool = new (std::nothrow) Pool(workers);
+  if (!m->submit_pool || !m->collect_pool) {
+    tbg_multi_destroy(m);
+    return TBG_E_OOM;
+  }
   *out = m;
   return TBG_OK;
 }
 
 void tbg_multi_destroy(tbg_multi* m) {
   if (!m) return;
+  delete m->submit_pool;  // (joins the workers: no call may be in flight)
+  delete m->collect_pool;
   for (auto* x : m->ctx) tbg_destroy(x);
   delete m;
 }
@@ -175,7 +258,9 @@ int tbg_multi_load_pubkeys(tbg_multi* m, const uint8_t* pk48, uint32_t count, ui
   std::vector<uint32_t> first(n, 0);
   // The same table decoded on every device (in parallel); the status of
   // context 0 is reported (every device computes the same one).
-  parallel_for(n, [&](uint32_t i) { rc[i] = tbg_load_pubkeys(m->ctx[i], pk48, count, &first[i], i == 0 ? status : nullptr); });
+  m->submit_pool->run(n, [&](uint32_t i) {
+    rc[i] = tbg_load_pubkeys(m->ctx[i], pk48, count, &first[i], i == 0 ? status : nullptr);
+  });
   for (uint32_t i = 0; i < n; ++i)
     if (rc[i] != TBG_OK) return rc[i];
   for (uint32_t i = 1; i < n; ++i)
@@ -190,6 +275,7 @@ int tbg_multi_submit(tbg_multi* m, const tbg_batch* b, tbg_ticket* ticket) {
 
 int tbg_multi_submit_group(tbg_multi* m, const tbg_batch* const* bs, uint32_t n_batches, tbg_ticket* tickets) {
   if (!m || !bs || !tickets || n_batches == 0) return TBG_E_INVALID_ARG;
+  const uint64_t t_call = now_ns();
   for (uint32_t k = 0; k < n_batches; ++k) {
     const int rc = validate_split(bs[k]);
     if (rc != TBG_OK) return rc;
@@ -245,14 +331,16 @@ int tbg_multi_submit_group(tbg_multi* m, const tbg_batch* const* bs, uint32_t n_
     if (!pieces[i].empty()) use.push_back(i);
   std::vector<int> src(use.size(), TBG_OK);
   std::vector<std::vector<tbg_ticket>> part_tickets(use.size());
-  parallel_for((uint32_t)use.size(), [&](uint32_t u) {
+  m->submit_pool->run((uint32_t)use.size(), [&](uint32_t u) {
     const uint32_t i = use[u];
+    const uint64_t t0 = now_ns();
     std::vector<SubBatch> sb(pieces[i].size());
     std::vector<const tbg_batch*> ptr(pieces[i].size());
     for (size_t j = 0; j < sb.size(); ++j) {
       sb[j].build(*bs[pieces[i][j].k], pieces[i][j].d0, pieces[i][j].d1);
       ptr[j] = &sb[j].b;
     }
+    m->host[2] += now_ns() - t0;
     part_tickets[u].resize(sb.size());
     src[u] = tbg_submit_group(m->ctx[i], ptr.data(), (uint32_t)ptr.size(), part_tickets[u].data());  // copies
   });
@@ -290,6 +378,9 @@ int tbg_multi_submit_group(tbg_multi* m, const tbg_batch* const* bs, uint32_t n_
     tickets[k] = m->next_ticket++;
     m->jobs.emplace(tickets[k], std::move(jobs[k]));
   }
+  m->host[0] += 1;
+  m->host[1] += NP;
+  m->host[3] += now_ns() - t_call;
   return TBG_OK;
 }
 
@@ -311,8 +402,9 @@ int tbg_multi_collect(tbg_multi* m, tbg_ticket t, int32_t* pst, int32_t* dst, ui
   }
   // Every shard's wait and copy-out runs on its own thread, straight into the
   // caller's arrays at the shard's offsets (caller order by construction).
+  const uint64_t t_call = now_ns();
   std::vector<int> rc(job->shards.size(), TBG_OK);
-  parallel_for((uint32_t)job->shards.size(), [&](uint32_t k) {
+  m->collect_pool->run((uint32_t)job->shards.size(), [&](uint32_t k) {
     const Shard& s = job->shards[k];
     rc[k] = tbg_collect(m->ctx[s.ctx], s.ticket, pst ? pst + s.p0 : nullptr, dst ? dst + s.d0 : nullptr,
                         agg ? agg + 96ull * s.d0 : nullptr, 1);
@@ -321,8 +413,26 @@ int tbg_multi_collect(tbg_multi* m, tbg_ticket t, int32_t* pst, int32_t* dst, ui
     std::lock_guard<std::mutex> lk(m->mu);
     m->jobs.erase(t);
   }
+  m->host[4] += 1;
+  m->host[5] += now_ns() - t_call;
   for (int r : rc)
     if (r != TBG_OK) return r;
+  return TBG_OK;
+}
+
+int tbg_multi_host_stats(tbg_multi* m, uint64_t* out16, int reset) {
+  if (!m || !out16) return TBG_E_INVALID_ARG;
+  for (int k = 0; k < 6; ++k) out16[k] = reset ? m->host[k].exchange(0) : m->host[k].load();
+  uint64_t sum[8] = {};
+  for (auto* x : m->ctx) {
+    uint64_t v[8];
+    const int rc = tbg_host_stats(x, v, reset);
+    if (rc != TBG_OK) return rc;
+    for (int k = 0; k < 8; ++k) sum[k] += v[k];
+  }
+  for (int k = 0; k < 8; ++k) out16[6 + k] = sum[k];
+  out16[14] = m->ctx.size();
+  out16[15] = 0;
   return TBG_OK;
 }
 

@@ -29,6 +29,10 @@ RLC_L0_AUTO, RLC_L0_ON, RLC_L0_OFF = 0, 1, 2   # tbg_config.rlc_batch
 GIDENT_OFF, GIDENT_L3, GIDENT_CHUNKS = 0, 1, 2  # tbg_config.gident
 SGB_AUTO, SGB_ON, SGB_OFF = 0, 1, 2           # tbg_config.subgroup_batch
 L0_NOT_RUN, L0_PASSED, L0_FAILED = 0, 1, 2     # tbg_fetch_level0
+HOST_STAT_KEYS = ["submits", "partials_submitted", "pack_ns", "enqueue_ns", "collects", "partials_collected",
+                  "gather_ns", "wait_ns"]
+MULTI_HOST_STAT_KEYS = ["submits", "partials", "build_ns", "submit_wall_ns", "collects", "collect_wall_ns"] + \
+    ["ctx_" + k for k in HOST_STAT_KEYS] + ["contexts", "reserved"]
 E_PENDING = -6
 
 
@@ -241,6 +245,12 @@ class Engine:
         self._check(self._lib.tbg_fetch_subgroup(self._h, ticket, _ptr(out)), "tbg_fetch_subgroup")
         return dict(zip(["groups", "failed"], out.tolist()))
 
+    def host_stats(self, reset=False) -> dict:
+        """Host-side work of this context's submit / collect calls (tbg_host_stats)."""
+        out = np.zeros(8, dtype=np.uint64)
+        self._check(self._lib.tbg_host_stats(self._h, _ptr(out), 1 if reset else 0), "tbg_host_stats")
+        return dict(zip(HOST_STAT_KEYS, out.tolist()))
+
     def slot_bytes(self, ticket) -> tuple:
         """(device bytes, pinned host bytes) of the slot holding the ticket's batch."""
         dev, pin = ctypes.c_uint64(), ctypes.c_uint64()
@@ -396,6 +406,14 @@ class MultiEngine:
         for ticket, (_, _, nd, np_) in zip(t.tolist(), built):
             self._keep[ticket] = (nd, np_)
         return t.tolist()
+
+    def host_stats(self, reset=False) -> dict:
+        """Host-side work of the multi-context's calls (tbg_multi_host_stats)."""
+        out = np.zeros(16, dtype=np.uint64)
+        rc = self._lib.tbg_multi_host_stats(self._h, _ptr(out), 1 if reset else 0)
+        if rc != 0:
+            raise EngineError(f"tbg_multi_host_stats: {self._lib.tbg_strerror(rc).decode()} ({rc})")
+        return dict(zip(MULTI_HOST_STAT_KEYS, out.tolist()))
 
     def layout(self, ticket) -> list:
         out = np.zeros(self.size + 1, dtype=np.uint32)

@@ -253,6 +253,13 @@ int tbg_fetch_fallback(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out8);
  * combinations (0: every signature was tested alone), groups that failed
  * (their members were then tested one by one)]. */
 int tbg_fetch_subgroup(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out2);
+/* Host-side work of the context's submit / collect calls since the last
+ * reset (reset != 0 zeroes the counters after reading): out8 = [submit
+ * calls, partials submitted, ns packing the callers' arrays into pinned
+ * staging, ns enqueueing (H2D, the kernel chain, D2H), collect calls,
+ * partials collected, ns gathering (copy-out of statuses / aggregates and
+ * the adaptive policies' counts), ns waiting for the device]. */
+int tbg_host_stats(tbg_ctx* ctx, uint64_t* out8, int reset);
 /* Footprint of the slot holding the ticket's batch: device bytes (input
  * arena + work arena) and pinned host bytes (staging both ways). */
 int tbg_slot_bytes(tbg_ctx* ctx, tbg_ticket ticket, uint64_t* device_bytes, uint64_t* pinned_bytes);
@@ -312,8 +319,8 @@ int tbg_last_timings(const tbg_ctx* ctx, float* ms8);
  * engine is initialised from the app wiring (app/app.go:321-488).
  *
  * Public keys are replicated: tbg_multi_load_pubkeys decodes the table on
- * every device (1 M DVs x 4 shares x 420 B ~ 1.7 GB, 0.6 % of a GPU's 288
- * GB), so any shard can reference any id and the ids are the same as for a
+ * every device (1 M DVs x 4 shares x 452 B ~ 1.8 GB, 0.6 % of a GPU's 288
+ * GB: pk, [x]pk and level 0's pair table, 4 x 112 B of affine G1, + status), so any shard can reference any id and the ids are the same as for a
  * single context.  Replication is the chosen design: the cut follows the
  * partial counts of whatever batches arrive (a burst of one committee's
  * duties still spreads over every GPU), where key-owned shards would route
@@ -340,6 +347,14 @@ int tbg_multi_submit_group(tbg_multi* m, const tbg_batch* const* batches, uint32
  * shard has finished (nothing is consumed before that). */
 int tbg_multi_collect(tbg_multi* m, tbg_ticket ticket, int32_t* partial_status, int32_t* duty_status,
                       uint8_t* agg96, int block);
+/* Host-side work of the multi-context's calls since the last reset (reset
+ * != 0 zeroes every counter, the contexts' too): out16 = [submit calls,
+ * partials submitted, ns building the per-context sub-batches (summed over
+ * the host workers), submit wall ns, collect calls, collect wall ns, then
+ * the 8 tbg_host_stats counters summed over the contexts (pack ns and
+ * gather ns are CPU time of the context's own thread), context count, 0].
+ * The cut / pack / gather run on persistent per-context host workers. */
+int tbg_multi_host_stats(tbg_multi* m, uint64_t* out16, int reset);
 /* Shard layout of a submitted (not yet collected) ticket: for shard i,
  * duty range [duty_lo[i], duty_lo[i+1]); arrays of tbg_multi_size()+1. */
 int tbg_multi_layout(tbg_multi* m, tbg_ticket ticket, uint32_t* duty_lo);

@@ -1028,6 +1028,13 @@ int hc_inv_bgcd(const uint8_t* a48, uint8_t* out48) {
   to_be(fp_canon(r), out48);
   return fp_eq(r, f) ? 0 : 1;
 }
+// the same value as a + p in [p, 2p) (device callers pass such values)
+int hc_inv_bgcd_plus_p(const uint8_t* a48, uint8_t* out48) {
+  const Fp a = from_be(a48);
+  const Fp r = fp_inv_bgcd(fp_add(a, fp_from_const(P_L))), f = fp_inv_fermat(a);
+  to_be(fp_canon(r), out48);
+  return fp_eq(r, f) ? 0 : 1;
+}
 }
 extern "C" {
 // The 68 -g1-folded lines of an affine G2 point (4 x 48-byte coordinates,
@@ -1054,5 +1061,64 @@ int hc_row_lines(const uint8_t* q192) {
     if (!fp_eq(a, b)) ++bad;
   }
   return bad;
+}
+}
+
+#include "../../charon_amd/csrc/bls_rlc.h"
+extern "C" {
+// The batched subgroup test's coefficients of partial i (sgb_digits).
+void hc_sgb_digits(const uint32_t* seed8, uint32_t i, int32_t* out18) {
+  uint32_t seed[8];
+  for (int k = 0; k < 8; ++k) seed[k] = seed8[k];
+  int32_t c[18];
+  sgb_digits(seed, i, c);
+  for (int k = 0; k < 18; ++k) out18[k] = c[k];
+}
+// k_sgb.hip's test of one group, lane pairs emulated (Fp2p): the n 96-byte
+// signatures of partials i0 .. i0 + n - 1 decoded WITHOUT the subgroup check
+// (a decode failure leaves the partial out, as in the kernels), the 18
+// bucket sums of each combination, Q_k by running sums, psi(Q_k) == [x] Q_k.
+// Returns the bit mask of the combinations that failed (-1: bad argument).
+int hc_sgb_group(const uint8_t* sigs96, int n, const uint32_t* seed8, uint32_t i0) {
+  if (n < 0 || n > 512) return -1;
+  uint32_t seed[8];
+  for (int k = 0; k < 8; ++k) seed[k] = seed8[k];
+  static G2A pts[512];
+  static bool ok[512];
+  for (int i = 0; i < n; ++i) ok[i] = g2_decompress_t<false, false>(sigs96 + 96 * i, pts[i]) == DEC_OK;
+  int mask = 0;
+  for (int k = 0; k < 18; ++k) {
+    Jac<Fp2p> bucket[6];
+    for (auto& b : bucket) b = jac_inf<Fp2p>();
+    for (int i = 0; i < n; ++i) {
+      if (!ok[i]) continue;
+      int32_t c[18];
+      sgb_digits(seed, i0 + (uint32_t)i, c);
+      if (!c[k]) continue;
+      Aff<Fp2p> p{pp_from(pts[i].x), f_reduce(pp_from(pts[i].y))};
+      if (c[k] < 0) p.y = f_reduce(f_neg(p.y));
+      bucket[(c[k] < 0 ? -c[k] : c[k]) - 1] = jac_add_aff_in(bucket[(c[k] < 0 ? -c[k] : c[k]) - 1], p);
+    }
+    Jac<Fp2p> run = jac_inf<Fp2p>(), q = run;
+    for (int v = 6; v >= 1; --v) {
+      run = jac_add_in<Fp2p, true>(run, bucket[v - 1]);
+      q = jac_add_in<Fp2p, true>(q, run);
+    }
+    bool pass = true;
+    if (!jac_is_inf(q)) {
+      bool exc = false;
+      const Jac<Fp2p> m = jac_mul_xabs_x(q, exc);
+      if (exc || jac_is_inf(m)) {
+        pass = false;
+      } else {
+        const Jac<Fp2p> ps = g2_psi_g(q);
+        const Fp2p z1 = f_sqr(ps.Z), z2 = f_sqr(m.Z);
+        pass = f_eq(f_mul(ps.X, z2), f_mul(m.X, z1)) &&
+               f_eq(f_mul(f_mul(ps.Y, m.Z), z2), f_reduce(f_neg(f_mul(f_mul(m.Y, ps.Z), z1))));
+      }
+    }
+    if (!pass) mask |= 1 << k;
+  }
+  return mask;
 }
 }

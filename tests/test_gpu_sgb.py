@@ -1,0 +1,109 @@
+"""The batched G2 subgroup test on the GPU (k_sgb.hip) against oracle/c.
+
+Signatures crafted against random combinations (tests/golden/sgb_points.json:
+13- and 23-torsion components, a bare torsion point, a pair whose components
+cancel in a plain sum) and a random non-subgroup point are placed at the
+first and last position of a group of 512 partials, two in one group, the
+cancelling pair in one group, and the last partial of a short final group.
+Every partial's status, every duty status and every aggregate must equal
+oracle/c's per-item schedule (tblsconv.SigFromCore's subgroup check,
+tblsconv/tblsconv.go:125-132, then tbls.VerifyAndAggregate), with the
+batched test forced on, forced off, and in its adaptive mode.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+M = 512  # SGB_M
+
+
+def crafted_batch(engine):
+    from tools.workload import invalid_pool, make_batch
+    with open(os.path.join(HERE, "golden", "sgb_points.json")) as f:
+        pts = {k: [bytes.fromhex(h) for h in v] for k, v in json.load(f)["points"].items()}
+    b = make_batch(engine, 1500, 3, 4, seed=4242)  # 6000 partials: 11 full groups + one of 368
+    n_p = len(b.sigs)
+    place = {
+        0: pts["t13"][0],                      # group 0, first member
+        M - 1: pts["t23"][0],                  # group 0, last member
+        M + 100: pts["torsion13"][0],          # group 1: two bad members
+        M + 300: pts["t13"][1],
+        2 * M + 7: pts["pair_a"][0],           # group 2: the cancelling pair
+        2 * M + 8: pts["pair_b"][0],
+        5 * M + 255: invalid_pool()["non_subgroup"][0],
+        n_p - 1: pts["t13"][2],                # the short last group, last member
+    }
+    sigs = np.array(b.sigs, copy=True)
+    for i, s in place.items():
+        sigs[i] = np.frombuffer(s, dtype=np.uint8)
+    b.sigs = sigs
+    return b, sorted(place)
+
+
+def run(engine, b):
+    from charon_amd import engine as eng
+    t = engine.submit(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
+                      duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
+    res = engine.collect(t)
+    return res, engine.subgroup(t)
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from charon_amd import engine as eng
+    es = {m: eng.Engine(0, slots=1, subgroup_batch=m) for m in (eng.SGB_ON, eng.SGB_OFF, eng.SGB_AUTO)}
+    yield es
+    for e in es.values():
+        e.close()
+
+
+def test_crafted_points_match_oracle_batched_and_alone(engines):
+    from charon_amd import engine as eng
+    from tests.test_gpu_fullsize import assert_same, oracle_run
+    e_on, e_off = engines[eng.SGB_ON], engines[eng.SGB_OFF]
+    b, bad = crafted_batch(e_on)
+    res, sg = run(e_on, b)
+    ref = oracle_run(b)
+    assert_same(res, ref)
+    assert np.flatnonzero(res.partial_status == eng.PS_ERR_SUBGROUP).tolist() == bad
+    n_sg = (len(b.sigs) + M - 1) // M
+    # groups 0, 1, 2, 5 and the last failed; every other group passed whole
+    assert sg == {"groups": n_sg, "failed": 5}, sg
+    # the same batch with every signature tested alone: identical results
+    b2, _ = crafted_batch(e_off)
+    res2, sg2 = run(e_off, b2)
+    assert sg2["groups"] == 0
+    assert np.array_equal(res2.partial_status, res.partial_status)
+    assert np.array_equal(res2.duty_status, res.duty_status) and np.array_equal(res2.agg, res.agg)
+
+
+def test_adaptive_mode_turns_off_and_on(engines):
+    from charon_amd import engine as eng
+    from tools.workload import make_batch
+    e = engines[eng.SGB_AUTO]
+    b, bad = crafted_batch(e)
+    res, sg = run(e, b)  # first batch: clean history, batched
+    assert sg["groups"] > 0 and sg["failed"] == 5
+    assert np.flatnonzero(res.partial_status == eng.PS_ERR_SUBGROUP).tolist() == bad
+    # 8 / 6000 non-subgroup partials: the average passes TBG_SGB_AUTO_MAX, the next batch tests alone
+    clean = make_batch(e, 1500, 3, 4, seed=4343)
+    res, sg = run(e, clean)
+    assert sg["groups"] == 0 and (res.partial_status == eng.PS_VALID).all()
+    # clean batches bring the average back under the bound
+    for _ in range(4):
+        res, sg = run(e, clean)
+    assert sg["groups"] > 0 and sg["failed"] == 0 and (res.partial_status == eng.PS_VALID).all()
+
+
+def test_small_batches_test_each_signature(engines):
+    from charon_amd import engine as eng
+    from tools.workload import make_batch
+    e = engines[eng.SGB_ON]
+    b = make_batch(e, 200, 3, 4, seed=4444)  # 800 partials < 2 groups: no batched test
+    res, sg = run(e, b)
+    assert sg["groups"] == 0 and (res.partial_status == eng.PS_VALID).all()

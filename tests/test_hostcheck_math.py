@@ -567,6 +567,11 @@ def test_bernstein_yang_inversion():
         rc = lib().hc_inv_bgcd(be(v), ob)
         assert rc == 0, v
         assert fe(ob.raw) == (pow(v, P - 2, P) if v else 0)
+        # the Montgomery form of v plus p, in [p, 2p) as device callers pass it
+        # (v = p - 1 gives 2p - 1's representative)
+        rc = lib().hc_inv_bgcd_plus_p(be(v), ob)
+        assert rc == 0, v
+        assert fe(ob.raw) == (pow(v, P - 2, P) if v else 0)
 
 
 def test_row_g2_lines_match_lane_lines():

@@ -131,11 +131,26 @@ def main():
     duty_sum4 -= saved
     rlc_partial -= saved  # (k_rlc_partial2: the n2 inversion batched; its G1 product now from the key's table)
     hash_ -= 2 * saved
+    # batched subgroup test (k_sgb.hip, SGB_M = 512, 18 combinations with
+    # digits uniform mod 13: 12/13 of them non-zero): per partial 18 * 12 / 13
+    # mixed additions into buckets; per group and combination the running
+    # sums over 6 buckets x 4 slices (30 additions) and one psi(Q) == [x]Q
+    # test on a Jacobian Q (the affine test with its 5 mixed additions full)
+    madd, _ = measure(lib.hc_k_msm_entry, 0)  # k = 0: psi^0, one mixed addition
+    sgb_m, sgb_k = 512, 18
+    sgb_bucket = sgb_k * 12 / 13 * madd
+    sgb_combine = sgb_k * 30 * g2_add / sgb_m
+    sgb_test = sgb_k * (k_subgroup + 5 * (g2_add - madd)) / sgb_m
+    sgb_per_partial = sgb_bucket + sgb_combine + sgb_test
+    decode_sgb = k_decode + sgb_per_partial
     l0_per_group = nch * chunk2 + nch * qmul
     l0_per_launch = bucket_scales + (32768 + 2048 + 128 + 8) * g2_add + lines_h + s_quad + final1
     launch_dvs = 16 * 10000  # bench default: 16 batches of 10k DVs per launch
-    unit_3of4_l0 = (4 * decode + hash_ + lines_h + 4 * l0_partial + duty_sum_p4 + l0_per_group / G + agg
-                    + l0_per_launch / launch_dvs)
+    unit_3of4_l0_alone = (4 * decode + hash_ + lines_h + 4 * l0_partial + duty_sum_p4 + l0_per_group / G + agg
+                          + l0_per_launch / launch_dvs)
+    # the default chain: decode + the batched subgroup test instead of one
+    # subgroup test per signature
+    unit_3of4_l0 = unit_3of4_l0_alone - 4 * decode + 4 * decode_sgb
     # every candidate but the first of each group is randomised: (4 G - 1) / G per duty
     unit_3of4_rlc = (4 * decode + hash_ + lines_h + (4 * G - 1) / G * rlc_partial + duty_sum4 + group_lines8 / G
                      + rlc_check_per_group / G + agg)
@@ -155,6 +170,8 @@ def main():
                  "l0_per_launch": round(l0_per_launch), "l0_bucket_scales": round(bucket_scales),
                  "g2_add": g2_add, "quad_mul": qmul, "l0_s_quad": s_quad, "final_exp_quad": final1,
                  "unit_3of4_l0": round(unit_3of4_l0), "l0_launch_dvs": launch_dvs,
+                 "unit_3of4_l0_subgroup_alone": round(unit_3of4_l0_alone),
+                 "decode_sig_batched_subgroup": round(decode_sgb), "sgb_per_partial": round(sgb_per_partial),
                  "unit_3of4_rlc": round(unit_3of4_rlc), "unit_3of4_each": unit_3of4,
                  "unit_3of4_single_lane_schedule": unit_3of4_v1},
         "fp_mul_equiv": {k: round(v / 392, 1) for k, v in
@@ -166,6 +183,7 @@ def main():
                           "aggregate_3of4_all4": agg, "l0_partial": l0_partial, "l0_duty_sum_4": duty_sum_p4,
                           "l0_per_group": l0_per_group, "l0_per_launch": l0_per_launch,
                           "unit_3of4_l0": unit_3of4_l0, "unit_3of4_rlc": unit_3of4_rlc,
+                          "decode_sig_batched_subgroup": decode_sgb,
                           "unit_3of4_each": unit_3of4, "unit_3of4_reference_schedule": unit_3of4_v1}.items()},
         "verify_hbm_bytes_per_launch": None,
         "batched_inversion": {"fp_inv": fp_inv_cost, "per_value_in_workgroups_of_256": round(binv_item, 1)},
@@ -174,6 +192,9 @@ def main():
         "kernels": {
             "k_decode_sigs": {"per": "partial", "mads": round(k_decode)},
             "k_subgroup_sigs": {"per": "partial", "mads": round(k_subgroup)},
+            "k_sgb_bucket": {"per": "partial", "mads": round(sgb_bucket)},
+            "k_sgb_combine": {"per": "partial", "mads": round(sgb_combine)},
+            "k_sgb_test": {"per": "partial", "mads": round(sgb_test)},
             "k_hash_map": {"per": "message", "mads": round(k_hash_map)},
             "k_hash_clear_x1": {"per": "message", "mads": round(k_clear_x1)},
             "k_hash_clear_x2": {"per": "message", "mads": round(k_clear_x2)},
