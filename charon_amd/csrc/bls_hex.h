@@ -262,8 +262,9 @@ TBG_DEV Fp4h hex_line_mul(const Fp4h& A, const uint32_t* l0_src, Fp2o l0, const 
 
 // f *= line(idx) of stored (unevaluated) lines at affine P = (-x, y): lane
 // (0, c) evaluates l1_c (-x), lane (1, c) l4_c y; the trio broadcasts them
-// and the pair swaps the other components
-TBG_DEV Fp4h hex_line_at(const Fp4h& A, const uint32_t* lines, int idx, const Fp& nx, const Fp& y) {
+// and the pair swaps the other components.  `v` is this lane's operand:
+// -x on q = 0, y on q = 1 (q = 2: any, its product is not used).
+TBG_DEV Fp4h hex_line_at_v(const Fp4h& A, const uint32_t* lines, int idx, const Fp& v) {
   const uint32_t c = hex_c();
   const int q = quad_lane();
   const uint32_t* src = lines + LINE_WORDS * idx;
@@ -271,10 +272,15 @@ TBG_DEV Fp4h hex_line_at(const Fp4h& A, const uint32_t* lines, int idx, const Fp
   const int k = q == 0 ? 2 : 4;
 #pragma unroll
   for (int i = 0; i < NL; ++i) lk.l[i] = src[(k + (int)c) * NL + i];
-  const Fp e = fp_mul(lk, fp_select(q == 0, nx, y));
+  const Fp e = fp_mul(lk, v);
   const Fp e1 = xch<QP_B0>(e), e4 = xch<QP_B1>(e);
   return hex_line_mul(A, src, Fp2o{}, Fp2o{e1, hx_swap(e1)}, Fp2o{e4, hx_swap(e4)});
 }
+TBG_DEV Fp4h hex_line_at(const Fp4h& A, const uint32_t* lines, int idx, const Fp& nx, const Fp& y) {
+  return hex_line_at_v(A, lines, idx, fp_select(quad_lane() == 0, nx, y));
+}
+// this lane's evaluation operand of a point stored as (-x, y) (one Fp loaded)
+TBG_DEV Fp hex_line_operand(const G1A& P) { return quad_lane() == 0 ? P.x : P.y; }
 // f *= line(idx) of folded (already evaluated) lines
 TBG_DEV Fp4h hex_line_folded(const Fp4h& A, const uint32_t* lines, int idx) {
   const uint32_t c = hex_c();

@@ -25,8 +25,14 @@ __device__ __forceinline__ Jac<Fp2x> px_psi(const Jac<Fp2x>& p) {
   return {f_mulc(f_conj(p.X), PSI_X), f_mulc(f_conj(p.Y), PSI_Y), f_reduce(f_conj(p.Z))};
 }
 
-// [x] p = -[|x|] p (63 doublings, 5 additions; the P == Q case doubles inline)
-__device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
+// [x] p = -[|x|] p (63 doublings, 5 additions).  TBG_CLEAR_X: the additions
+// without the doubling case (bls_pair.h jac_mul_xabs_x: inputs retired early,
+// fewer live values), the rare doubling case (only points of tiny order)
+// redone with the complete formulas; 0: the complete formulas throughout.
+#ifndef TBG_CLEAR_X
+#define TBG_CLEAR_X 1
+#endif
+__device__ __forceinline__ Jac<Fp2x> px_mul_x_full(const Jac<Fp2x>& p) {
   Jac<Fp2x> acc = p;
 #pragma unroll 1
   for (int i = 62; i >= 0; --i) {
@@ -34,6 +40,14 @@ __device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
     if ((X_ABS >> i) & 1) acc = jac_add_in<Fp2x, true>(acc, p);
   }
   return jac_neg(acc);
+}
+__device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
+#if TBG_CLEAR_X
+  bool exc = false;
+  const Jac<Fp2x> acc = jac_mul_xabs_x(p, exc);
+  if (pair_all(!exc)) return jac_neg(acc);  // (pair-uniform)
+#endif
+  return px_mul_x_full(p);
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x1(DevBatch B) {

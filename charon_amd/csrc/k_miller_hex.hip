@@ -93,9 +93,7 @@ TBG_DEV Fp4h hex_pf_step(const Fp4h& A, const DevBatch& B, uint32_t d, uint32_t 
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t base = (lane & ~16u) - (uint32_t)q;  // lane (0, 0) of this hexad
   // this lane's G1 operand: -x_P on q = 0, y_P on q = 1 (q = 2: unused)
-  const G1A& P = B.dv_p[d];
-  const Fp v = q == 0 ? P.x : P.y;
-  const Fp nv = fp_select(q == 0, fp_reduce(fp_neg(v)), v);
+  const Fp nv = hex_line_operand(B.dv_p[d]);
   // lk = l1_c (q = 0) or l4_c (q = 1, 2), staged by lane (1, c) / (2, c)
   const Fp lk = hex_pf_read<BUF>(base + (q == 0 ? 1u : 2u) + (c << 4));
   const Fp e = fp_mul(lk, nv);
@@ -246,8 +244,7 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_miller_hex(DevBatch B) {
 #pragma unroll 1
         for (uint32_t bits = run; bits; bits &= bits - 1) {
           const uint32_t j = __builtin_ctz(bits);
-          const G1A& P = B.dv_p[d0 + j];
-          f = hex_line_at(f, B.h_lines + (size_t)LINES_WORDS * my_msg[j], idx, fp_reduce(fp_neg(P.x)), P.y);
+          f = hex_line_at_v(f, B.h_lines + (size_t)LINES_WORDS * my_msg[j], idx, hex_line_operand(B.dv_p[d0 + j]));
         }
         continue;
       }
@@ -257,8 +254,7 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_miller_hex(DevBatch B) {
         if (B.dv_state[d] != RLC_COMBINED) continue;
         const uint32_t m = B.duty_msg[d];
         if (B.h_status[m] != 0) continue;  // the check fails in k_l0_fold / k_rlc_group_final
-        const G1A& P = B.dv_p[d];
-        f = hex_line_at(f, B.h_lines + (size_t)LINES_WORDS * m, idx, fp_reduce(fp_neg(P.x)), P.y);
+        f = hex_line_at_v(f, B.h_lines + (size_t)LINES_WORDS * m, idx, hex_line_operand(B.dv_p[d]));
       }
     }
   }

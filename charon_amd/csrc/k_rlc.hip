@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_rlc_duty_sum(DevBatch B) {
     if (phase == DSUM_L0_P) B.counters[CNT_L0_BAD] = 1;
     return;
   }
-  B.dv_p[d] = Pa;
+  B.dv_p[d] = G1A{fp_reduce(fp_neg(Pa.x)), Pa.y};  // (-x, y): the Miller steps' evaluation operands
   if (phase == DSUM_BOTH) B.dv_s[d] = S;
   B.dv_state[d] = RLC_COMBINED;
 }
@@ -528,9 +528,12 @@ __global__ void TBG_LAUNCH k_rlc_cident_lines(DevBatch B) {
   for (uint32_t d = d0; d < d1; ++d) {
     if (!rlc_combinable(B, d)) continue;
     ++w;
-    G1A wp = B.dv_p[d];
-    if (w > 1) jac_to_aff(jac_mul_u64(jac_from_aff(wp), w), wp);  // w < r: never the identity
-    wp.x = fp_reduce(fp_neg(wp.x));
+    G1A wp = B.dv_p[d];  // (-x, y)
+    if (w > 1) {
+      wp.x = fp_reduce(fp_neg(wp.x));
+      jac_to_aff(jac_mul_u64(jac_from_aff(wp), w), wp);  // w < r: never the identity
+      wp.x = fp_reduce(fp_neg(wp.x));
+    }
     B.cid_p[(size_t)C * j + (w - 1)] = wp;
   }
   B.pend_pts[j] = Sa;  // lines: k_lines_fold<FOLD_CID>

@@ -79,7 +79,7 @@ struct DevBatch {
                           // chunk index `chunks` of a group is its S pair alone
   uint32_t* chunk_list;   // [n_groups * chunks] level-1.5 chunks of failed groups (group * chunks + c)
   uint32_t* chunk_lines;  // [fb window][LINES_WORDS] lines of S_c, by chunk-list position - fb_base
-  G1A* dv_p;              // [n_duties] sum r_i pk_i (affine)
+  G1A* dv_p;              // [n_duties] sum r_i pk_i (affine), stored as (-x, y)
   G2J* dv_s;              // [n_duties] sum r_i sig_i
   int32_t* dv_state;      // [n_duties] RLC_*
   int32_t* grp_state;     // [n_groups] GRP_*
