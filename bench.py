@@ -314,11 +314,12 @@ def latency_probe(e_load, eng, load_plan, sizes=(1, 64, 1024, 10000), reps=(30, 
     checked; the first call of each size (arena allocation) is not counted."""
     import threading
     from tools.workload import make_batch
-    e = eng.Engine(e_load.device, slots=2)
+    e = eng.Engine(e_load.device, slots=2)  # + the express slot (tbg_config.express_partials)
+    e_plain = eng.Engine(e_load.device, slots=2, express_partials=eng.EXPRESS_OFF)
     try:
-        bs = {n: make_batch(e, n, 3, 4, seed=7000 + n) for n in sizes}
+        bs = {n: make_batch(e, n, 3, 4, seed=7000 + n, load=lambda pk: _load_both(e, e_plain, pk)) for n in sizes}
 
-        def one(b):
+        def one(b, e=e):
             t0 = time.perf_counter()
             r = e.run(eng.OP_VERIFY_AGGREGATE, b.duty_first, b.sigs, b.identifiers, msgs=(b.msg_data, b.msg_off),
                       duty_msg=b.duty_msg, pubkey_ids=b.pubkey_ids, duty_threshold=b.threshold)
@@ -327,11 +328,11 @@ def latency_probe(e_load, eng, load_plan, sizes=(1, 64, 1024, 10000), reps=(30, 
                 raise RuntimeError("latency probe: result differs")
             return dt
 
-        def series():
+        def series(e=e):
             out = {}
             for n, k in zip(sizes, reps):
-                one(bs[n])
-                t = np.array([one(bs[n]) for _ in range(k)])
+                one(bs[n], e)
+                t = np.array([one(bs[n], e) for _ in range(k)])
                 out[str(n)] = {"p50_ms": round(float(np.percentile(t, 50)), 3),
                                "p99_ms": round(float(np.percentile(t, 99)), 3), "samples": k}
             return out
@@ -348,14 +349,26 @@ def latency_probe(e_load, eng, load_plan, sizes=(1, 64, 1024, 10000), reps=(30, 
         try:
             time.sleep(0.2)
             loaded = series()
+            loaded_plain = series(e_plain)
         finally:
             stop.set()
             th.join()
-        return {"idle": idle, "under_headline_load": loaded,
-                "path": "tbg_submit + tbg_collect of one VERIFY_AGGREGATE batch (3-of-4) on its own context; "
-                        "load = the headline launches replayed on another context of the same GPU"}
+        return {"idle": idle, "under_headline_load": loaded, "under_headline_load_no_express": loaded_plain,
+                "path": "tbg_submit + tbg_collect of one VERIFY_AGGREGATE batch (3-of-4) on its own context "
+                        "(batches up to 4096 partials on its high-priority express slot; *_no_express: a context "
+                        "without one); load = the headline launches replayed on another context of the same GPU"}
     finally:
         e.close()
+        e_plain.close()
+
+
+def _load_both(e1, e2, pk):
+    """Load pubshares into two contexts at the same ids (the latency probe's
+    batches run on either)."""
+    f1, st = e1.load_pubkeys(pk)
+    f2, _ = e2.load_pubkeys(pk)
+    assert f1 == f2
+    return f1, st
 
 
 def batch_exact(res, b, eng):

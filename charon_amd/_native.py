@@ -184,6 +184,7 @@ class TbgConfig(ctypes.Structure):
         ("gident", ctypes.c_uint32),
         ("fb_window", ctypes.c_uint32),
         ("subgroup_batch", ctypes.c_uint32),
+        ("express_partials", ctypes.c_uint32),
     ]
 
 

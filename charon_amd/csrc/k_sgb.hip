@@ -110,21 +110,26 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_bucket(DevBatch B, uint32_t n
 
 // one lane pair per (group, combination): Q_k = sum_v v B_v by running sums
 // from v = 6 down, stored over the combination's first slice (only this pair
-// reads those slices)
+// reads those slices).  The additions skip the doubling case (bls_pair.h
+// jac_add_x: fewer live values than the complete formulas): two equal
+// partial sums -- which random digits make negligible -- fail the group,
+// whose members are then tested one by one.
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_combine(DevBatch B, uint32_t n_sg) {
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (w >= n_sg * SGB_K) return;
   const uint32_t g = w / SGB_K, k = w % SGB_K;
   G2J* part = B.sgb_part + ((size_t)SGB_BUCKETS * g + (size_t)SGB_V * k) * SGB_SPLIT;
   Jac<Fp2x> run = jac_inf<Fp2x>(), q = run;
+  bool exc = false;
 #pragma unroll 1
   for (int v = (int)SGB_V; v >= 1; --v) {
     const G2J* pb = part + (size_t)(v - 1) * SGB_SPLIT;
 #pragma unroll 1
-    for (uint32_t sl = 0; sl < SGB_SPLIT; ++sl) run = jac_add_in<Fp2x, true>(run, px_load(pb[sl]));
-    q = jac_add_in<Fp2x, true>(q, run);
+    for (uint32_t sl = 0; sl < SGB_SPLIT; ++sl) run = jac_add_x(run, px_load(pb[sl]), exc);
+    q = jac_add_x(q, run, exc);
   }
-  px_store(part[0], q);
+  if (pair_all(!exc)) px_store(part[0], q);
+  else if (pair_par() == 0) B.sgb_bad[g] = 1u;
 }
 
 // one lane pair per (group, combination): psi(Q) == [x] Q; a failure (or the

@@ -77,6 +77,7 @@ struct Part {
 
 struct Slot {
   bool busy = false;        // some part is still pending
+  bool express = false;     // the high-priority slot of small batches (tbg_config.express_partials)
   std::vector<Part> parts;
   tbg_ticket ticket = 0;    // first part's ticket (LRU order of the slots)
   uint32_t op = 0, n_duties = 0, n_partials = 0, n_msgs = 0;
@@ -123,6 +124,7 @@ struct tbg_ctx {
   // exponentiations and Fp12 squarings per duty.
   uint32_t rlc_group = 16;  // 0 = per-partial checks (TBG_VERIFY_EACH)
   uint32_t rlc_chunk = 4;
+  bool chunk_auto = true;    // rlc_chunk not configured: level-0 launches of many duties take 8
   bool rlc_auto = false;     // rlc_group follows the observed invalid share (tbg_config.rlc_group = 0)
   uint32_t rlc_batch = TBG_RLC_L0_AUTO;  // level 0 (the whole device batch as one check)
   double invalid_ema = 0.0;  // exponential average of the invalid share of collected verified partials
@@ -131,6 +133,7 @@ struct tbg_ctx {
   uint32_t gident = TBG_GIDENT_OFF;  // level 1g routing (tbg_config.gident)
   uint32_t fb_window = TBG_FB_WINDOW;  // fallback line buffer positions per pass (tbg_config.fb_window)
   uint32_t sgb_mode = TBG_SGB_AUTO;    // batched subgroup test (tbg_config.subgroup_batch)
+  uint32_t express_max = TBG_EXPRESS_PARTIALS;  // batches up to this many partials prefer the express slot
   // host-side work of the submit / collect calls (tbg_host_stats): [submits,
   // partials submitted, pack ns, enqueue ns, collects, partials collected,
   // gather ns, wait ns]
@@ -211,7 +214,10 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   else if (cfg && cfg->verify_mode != TBG_VERIFY_RLC) { delete c; return TBG_E_INVALID_ARG; }
   else if (cfg && cfg->rlc_group) c->rlc_group = cfg->rlc_group;
   else c->rlc_auto = true;
-  if (cfg && cfg->rlc_chunk) c->rlc_chunk = cfg->rlc_chunk;
+  if (cfg && cfg->rlc_chunk) {
+    c->rlc_chunk = cfg->rlc_chunk;
+    c->chunk_auto = false;
+  }
   if (c->rlc_group > 4096 || c->rlc_chunk > 4096) { delete c; return TBG_E_INVALID_ARG; }
   if (cfg && cfg->rlc_batch > TBG_RLC_L0_OFF) { delete c; return TBG_E_INVALID_ARG; }
   if (cfg) c->rlc_batch = cfg->rlc_batch;
@@ -221,6 +227,7 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   if (cfg && cfg->fb_window) c->fb_window = cfg->fb_window;
   if (cfg && cfg->subgroup_batch > TBG_SGB_OFF) { delete c; return TBG_E_INVALID_ARG; }
   if (cfg) c->sgb_mode = cfg->subgroup_batch;
+  if (cfg && cfg->express_partials) c->express_max = cfg->express_partials;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->retire_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->keys_ready, hipEventDisableTiming) != hipSuccess) {
@@ -234,14 +241,16 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // other leaves idle).
   uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 3;
   const uint32_t spp = (cfg && cfg->streams_per_slot > 1) ? cfg->streams_per_slot : 1;
-  if (nslots > TBG_MAX_SLOTS || spp > 2 || nslots * spp > TBG_MAX_SLOT_STREAMS) {
+  const bool express = c->express_max != TBG_EXPRESS_OFF;
+  if (nslots > TBG_MAX_SLOTS || spp > 2 || nslots * spp + (express ? 1 : 0) > TBG_MAX_SLOT_STREAMS) {
     hipStreamDestroy(c->stream);
     hipEventDestroy(c->retire_ev);
     hipEventDestroy(c->keys_ready);
     delete c;
     return TBG_E_INVALID_ARG;
   }
-  c->slots.resize(nslots);
+  // (+ the express slot: one more slot, last, on a high-priority stream)
+  c->slots.resize(nslots + (express ? 1 : 0));
   // One stream per slot by default: the HIP runtime maps streams onto a
   // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), so concurrency
   // comes from several batches in flight, one queue each.  Two streams
@@ -249,14 +258,28 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // single-batch latency when queues are plentiful).
   const bool two = cfg && cfg->streams_per_slot >= 2;
   // (Per-slot stream priorities were measured within noise, round 3.)
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = prio_least = 0;
   for (size_t k = 0; k < c->slots.size(); ++k) {
     auto& s = c->slots[k];
+    s.express = express && k == nslots;
     auto mk = [&](hipStream_t* st) { return hipStreamCreateWithFlags(st, hipStreamNonBlocking); };
-    if (mk(&s.st) != hipSuccess || (two && mk(&s.st2) != hipSuccess)) {
-      tbg_destroy(c);
-      return TBG_E_DEVICE;
+    if (s.express) {
+      // A small batch's chain is ~50 short kernels in series: on a
+      // high-priority queue their dispatches go ahead of the throughput
+      // launches' pending workgroups instead of queueing behind them.
+      if (hipStreamCreateWithPriority(&s.st, hipStreamNonBlocking, prio_greatest) != hipSuccess) {
+        tbg_destroy(c);
+        return TBG_E_DEVICE;
+      }
+      s.st2 = s.st;
+    } else {
+      if (mk(&s.st) != hipSuccess || (two && mk(&s.st2) != hipSuccess)) {
+        tbg_destroy(c);
+        return TBG_E_DEVICE;
+      }
+      if (!two) s.st2 = s.st;
     }
-    if (!two) s.st2 = s.st;
     for (auto& e : s.ev) hipEventCreate(&e);
     hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
   }
@@ -530,10 +553,15 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   std::unique_lock<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   // Least recently used free slot: a collected batch stays resident (for
-  // tbg_replay / tbg_fetch) until every other slot has been reused.
+  // tbg_replay / tbg_fetch) until every other slot has been reused.  A batch
+  // of at most express_max partials takes the express slot when it is free.
   Slot* s = nullptr;
+  const bool small = np64 <= c->express_max;
   for (auto& x : c->slots)
-    if (!x.busy && (!s || x.ticket < s->ticket)) s = &x;
+    if (x.express && small && !x.busy) s = &x;
+  if (!s)
+    for (auto& x : c->slots)
+      if (!x.express && !x.busy && (!s || x.ticket < s->ticket)) s = &x;
   if (!s) return TBG_E_BUSY;
 
   const uint32_t nd = (uint32_t)nd64, np = (uint32_t)np64, nm = (uint32_t)nm64;
@@ -569,12 +597,22 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
     c->rlc_group = c->invalid_ema < TBG_RLC_AUTO_TO8 ? 16 : c->invalid_ema < TBG_RLC_AUTO_TO4 ? 8 : 4;
   const uint32_t G = verify ? c->rlc_group : 0;
   const uint32_t ng = G ? (nd + G - 1) / G : 0;
-  const uint32_t C = c->rlc_chunk < G ? c->rlc_chunk : (G ? G : 1);
-  const uint32_t nch = G ? (G + C - 1) / C : 0;
   // Level 0 while the collected batches are clean (or as configured): one
   // failed level-0 check costs its own work on top of the group levels.
   const bool l0 = G != 0 && np < (1u << 28) &&
                   (c->rlc_batch == TBG_RLC_L0_ON || (c->rlc_batch == TBG_RLC_L0_AUTO && c->invalid_ema < TBG_RLC_AUTO_L0));
+  // Duties per Miller hexad: 4, or 8 for a level-0 launch of at least
+  // TBG_CHUNK8_DUTIES duties (unless tbg_config.rlc_chunk fixes it).  The
+  // level-0 Miller kernel's waves are long (the whole 68-step loop, ~6 ms),
+  // so a launch whose waves fill 1.5 rounds of the 2,048 two-wave slots
+  // runs two: config 4's 125k-DV shard at C = 4 is 3,126 waves (frac 0.49
+  // against 0.61 for the 160k-DV headline launch's 4,001, VERDICT r04 item
+  // 4).  At C = 8 a launch of n duties is ~n / 80 waves with half the
+  // squarings per duty: one round from ~120k duties on.
+  uint32_t Cw = c->rlc_chunk;
+  if (c->chunk_auto && l0 && nd >= TBG_CHUNK8_DUTIES) Cw = 8;
+  const uint32_t C = Cw < G ? Cw : (G ? G : 1);
+  const uint32_t nch = G ? (G + C - 1) / C : 0;
   size_t w_pp = sec(G ? sizeof(G1J) * (size_t)np : 0);
   size_t w_ps = sec(G ? sizeof(G2J) * (size_t)np : 0);
   size_t w_cf = sec(G ? 4ull * 3 * 4 * NL * ng * (nch + 1) : 0);

@@ -13,6 +13,11 @@ namespace tbg {
 constexpr int kBlock = 64;
 // Default list positions per pass of the fallback levels' shared line buffer
 // (22.8 KB each: 0.75 GB per slot; tbg_config.fb_window overrides it).
+// Level-0 launches of at least this many duties run 8 duties per Miller
+// hexad instead of 4 (tbls_engine.hip, tbg_submit_group); 0xFFFFFFFF: never.
+#ifndef TBG_CHUNK8_DUTIES
+#define TBG_CHUNK8_DUTIES 120000u
+#endif
 #ifndef TBG_FB_WINDOW
 #define TBG_FB_WINDOW 32768u
 #endif

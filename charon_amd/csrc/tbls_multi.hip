@@ -218,6 +218,9 @@ int tbg_multi_init(const tbg_config* cfg, const int32_t* devices, uint32_t n_dev
   if (!m) return TBG_E_OOM;
   tbg_config c{};
   if (cfg) c = *cfg;
+  // no express slot unless asked for: n contexts' streams add up per process
+  // (TBG_MAX_SLOT_STREAMS)
+  if (c.express_partials == 0) c.express_partials = TBG_EXPRESS_OFF;
   for (uint32_t i = 0; i < n_devices; ++i) {
     c.device = devices[i];
     tbg_ctx* x = nullptr;

@@ -28,6 +28,7 @@ VERIFY_RLC, VERIFY_EACH = 0, 1
 RLC_L0_AUTO, RLC_L0_ON, RLC_L0_OFF = 0, 1, 2   # tbg_config.rlc_batch
 GIDENT_OFF, GIDENT_L3, GIDENT_CHUNKS = 0, 1, 2  # tbg_config.gident
 SGB_AUTO, SGB_ON, SGB_OFF = 0, 1, 2           # tbg_config.subgroup_batch
+EXPRESS_OFF = 0xFFFFFFFF                        # tbg_config.express_partials: no express slot
 L0_NOT_RUN, L0_PASSED, L0_FAILED = 0, 1, 2     # tbg_fetch_level0
 HOST_STAT_KEYS = ["submits", "partials_submitted", "pack_ns", "enqueue_ns", "collects", "partials_collected",
                   "gather_ns", "wait_ns"]
@@ -78,12 +79,14 @@ class Engine:
 
     def __init__(self, device: int = 0, slots: int = 3, verify_mode: int = VERIFY_RLC, rlc_group: int = 0,
                  rlc_seed: int = 0, rlc_chunk: int = 0, streams_per_slot: int = 0, rlc_batch: int = 0,
-                 gident: int = GIDENT_OFF, fb_window: int = 0, subgroup_batch: int = SGB_AUTO):
+                 gident: int = GIDENT_OFF, fb_window: int = 0, subgroup_batch: int = SGB_AUTO,
+                 express_partials: int = 0):
         self._lib = _native.load()
         cfg = _native.TbgConfig(device=device, max_partials=0, max_duties=0, max_msg_bytes=0, slots=slots,
                                 verify_mode=verify_mode, rlc_group=rlc_group, rlc_seed=rlc_seed,
                                 rlc_chunk=rlc_chunk, streams_per_slot=streams_per_slot, rlc_batch=rlc_batch,
-                                gident=gident, fb_window=fb_window, subgroup_batch=subgroup_batch)
+                                gident=gident, fb_window=fb_window, subgroup_batch=subgroup_batch,
+                                express_partials=express_partials)
         h = ctypes.c_void_p()
         rc = self._lib.tbg_init(ctypes.byref(cfg), ctypes.byref(h))
         self._check(rc, "tbg_init")

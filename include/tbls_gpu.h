@@ -111,7 +111,14 @@ typedef struct {
                            * below TBG_SGB_AUTO_MAX; TBG_SGB_ON always; TBG_SGB_OFF
                            * every signature alone.  Batches below 1024 partials
                            * always test each signature alone.                        */
+  uint32_t express_partials; /* batches of at most this many partials go to an extra
+                           * slot on a high-priority stream when it is free (a small
+                           * batch's ~50 short kernels then dispatch ahead of the
+                           * throughput launches' workgroups): 0 -> TBG_EXPRESS_PARTIALS,
+                           * TBG_EXPRESS_OFF -> no express slot                        */
 } tbg_config;
+#define TBG_EXPRESS_PARTIALS 4096u
+#define TBG_EXPRESS_OFF 0xFFFFFFFFu
 #define TBG_SGB_AUTO 0
 #define TBG_SGB_ON 1
 #define TBG_SGB_OFF 2
