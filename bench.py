@@ -168,13 +168,16 @@ def kernel_profile(prof):
     return out
 
 
-def launch_items(groups, G):
-    """Items of one device batch (the `merge` caller batches of a slot)."""
+def launch_items(groups, shape):
+    """Items of one device batch (the `merge` caller batches of a slot);
+    `shape` = Engine.shape of its last submit (duties per group / chunk)."""
     nd = sum(b.n_dv for b in groups)
     np_ = sum(len(b.identifiers) for b in groups)
     nm = sum(len(b.msg_off) - 1 for b in groups)
+    G = shape.get("group") or 16
     ng = -(-nd // G)  # level-1 groups are cut from the packed device batch
-    return {"partial": np_, "message": nm, "duty": nd, "group": ng, "launch": 1}
+    chunks = shape.get("chunks") or ng * -(-G // 4)
+    return {"partial": np_, "message": nm, "duty": nd, "group": ng, "chunk": chunks, "launch": 1}
 
 
 def kernel_roofline(wm, kp, items, tm, batches):
@@ -191,7 +194,8 @@ def kernel_roofline(wm, kp, items, tm, batches):
         return None
     k = dom if dom in model else priced[0]
     m = model[k]
-    mads = m["mads"] * items[m["per"]] + m.get("plus_per_launch", 0)
+    mads = m["mads"] * items[m["per"]] + sum(v * items[u] for u, v in m.get("plus", {}).items()) \
+        + m.get("plus_per_launch", 0)
     ms, launches = kp[k]
     ach = mads / (ms * 1e-3) / 1e12
     traffic = None
@@ -211,6 +215,7 @@ def kernel_roofline(wm, kp, items, tm, batches):
             "traffic": traffic, "traffic_unit": "bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, "
                                                 "profiles/traffic_latest.json)" if traffic is not None else None,
             "algorithmic_mads_per_launch": int(mads), "work_model": f"{m['mads']} mads per {m['per']}"
+            + "".join(f" + {v} per {u}" for u, v in m.get("plus", {}).items())
             + (f" + {m['plus_per_launch']} per launch" if m.get("plus_per_launch") else ""),
             "items_per_launch": items[m["per"]], "launch_ms": round(ms / launches, 4),
             "batches_per_launch": batches, "dominant_by_exclusive_time": dom,
@@ -219,11 +224,16 @@ def kernel_roofline(wm, kp, items, tm, batches):
                         "command: tools/roofline_from_trace.py"}
 
 
-def pipeline_roofline(wm, value, l0, t, n, sgb=True):
-    """roofline_pipeline: the whole chain, work model x rate (config 2 shape)."""
+def pipeline_roofline(wm, value, l0, t, n, sgb=True, items=None):
+    """roofline_pipeline: the whole chain, work model x rate (config 2 shape;
+    `items` = launch_items of one launch: its level-0 P chunks, when the
+    launch shape is not the model's G = 16, C = 4)."""
     if not wm or (t, n) != (3, 4):
         return None
-    unit = wm["mads"]["unit_3of4_l0" if l0 else "unit_3of4_rlc"]
+    mm = wm["mads"]
+    unit = mm["unit_3of4_l0" if l0 else "unit_3of4_rlc"]
+    if l0 and items and "l0_chunk_base" in mm:  # P-chunk hexads (+ their fold products) per duty
+        unit += (items["chunk"] / items["duty"] - 0.25) * (mm["l0_chunk_base"] + mm["quad_mul"])
     if not sgb:  # every signature's subgroup test alone
         unit += 4 * (wm["mads"]["decode_sig"] - wm["mads"]["decode_sig_batched_subgroup"])
     ach = value * unit / 1e12
@@ -627,6 +637,7 @@ def main():
     b = batches[0][0]
     flat = [x for g in batches for x in g]
     group_used = e.stats(tickets[0])["group_size"]  # before api_pipeline reuses the slots (tickets expire)
+    shape = e.shape(tickets[0])
     l0_state = e.level0(tickets[0])
     fallback = e.fallback(tickets[0])  # per-level fallback work of the slot's last run
     slot_dev, slot_pinned = e.slot_bytes(tickets[0])
@@ -643,10 +654,11 @@ def main():
     iso = {st: round(sum(kp[k][0] for k in ks if k in kp), 3) for st, ks in STAGE_KERNELS.items()}
     iso["total"] = round(sum(v[0] for v in kp.values()), 3)
     wm = work_model()
-    roofline = kernel_roofline(wm, kp, launch_items(batches[0], group_used or 16), traffic_model(), M)
+    items = launch_items(batches[0], shape)
+    roofline = kernel_roofline(wm, kp, items, traffic_model(), M)
     # the roofline is per GPU: whole-job rate / ranks against one GPU's peak
     roofline_pipeline = pipeline_roofline(wm, value / ws, l0_state == eng.L0_PASSED, args.t, args.n,
-                                          subgroup["groups"] > 0) \
+                                          subgroup["groups"] > 0, items) \
         if args.workload in ("config2", "config4") else None
     # (before api_pipeline: the load replays the resident launches)
     lat = latency_probe(e, eng, plan(3 * M)) if args.latency and rank == 0 and args.workload == "config2" else None
@@ -662,7 +674,7 @@ def main():
         "config": {"workload": WORKLOADS[args.workload].format(dvs=args.dvs, inject=args.inject),
                    "partials_per_step_per_gpu": int(len(b.identifiers)), "parallelism": f"shard{ws}",
                    "inflight_launches": args.inflight, "batches_per_launch": M,
-                   "rlc_group": group_used, "gident": args.gident, "subgroup_batch": args.subgroup_batch,
+                   "rlc_group": group_used, "rlc_chunk": shape["chunk"], "gident": args.gident, "subgroup_batch": args.subgroup_batch,
                    "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
         "fallback_levels": fallback,

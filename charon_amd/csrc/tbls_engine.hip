@@ -134,6 +134,7 @@ struct tbg_ctx {
   uint32_t fb_window = TBG_FB_WINDOW;  // fallback line buffer positions per pass (tbg_config.fb_window)
   uint32_t sgb_mode = TBG_SGB_AUTO;    // batched subgroup test (tbg_config.subgroup_batch)
   uint32_t express_max = TBG_EXPRESS_PARTIALS;  // batches up to this many partials prefer the express slot
+  uint32_t hex_slots = 2048;  // Miller-hexad waves the device runs at once (CUs x 4 SIMDs x TBG_HEX_WAVES)
   // host-side work of the submit / collect calls (tbg_host_stats): [submits,
   // partials submitted, pack ns, enqueue ns, collects, partials collected,
   // gather ns, wait ns]
@@ -251,6 +252,9 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   }
   // (+ the express slot: one more slot, last, on a high-priority stream)
   c->slots.resize(nslots + (express ? 1 : 0));
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n_cu > 0)
+    c->hex_slots = (uint32_t)n_cu * 4u * 2u;  // two hexad waves per SIMD (bls_hex.h TBG_HEX_WAVES)
   // One stream per slot by default: the HIP runtime maps streams onto a
   // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), so concurrency
   // comes from several batches in flight, one queue each.  Two streams
@@ -530,6 +534,37 @@ static Slot* find_ticket(tbg_ctx* c, tbg_ticket t, bool want_pending, Part** par
 
 int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) { return tbg_submit_group(c, &b, 1, ticket); }
 
+// Level-0 launch shape.  The level-0 Miller kernel's
+// waves are long (one hexad = the whole 68-step loop over C duties, ~6 ms)
+// and all alike, so a launch takes ceil(waves / slots) rounds of one hexad's
+// time: config 4's 125k-duty shard at (16, 4) is 3,126 waves, 1.53 rounds
+// of 2,048 two-wave slots, run as two.  A hexad of C duties costs 62
+// squarings + 68 C line products, 0.95 M + 1.39 M C u32 mul-adds
+// (profiles/work_model.json, l0_chunk_*), so fewer, longer hexads win where
+// they save a round:
+// (16, 8) halves the squarings and runs 160k duties in one round, (14, 7)
+// runs 125k in 0.87 of one.  Launches within one round at (16, 4) keep it;
+// a configured group size G keeps G (C = 4 or 8 only).
+static void l0_shape(uint32_t nd, uint32_t slots, bool g_free, uint32_t& G, uint32_t& C) {
+  const uint32_t cand[3][2] = {{g_free ? 16u : G, 4}, {g_free ? 16u : G, 8}, {14, 7}};
+  auto rounds = [&](uint32_t g, uint32_t ch) {
+    const uint64_t hexads = (uint64_t)((nd + g - 1) / g) * ((g + ch - 1) / ch);
+    return ((hexads + 9) / 10 + slots - 1) / slots;
+  };
+  const uint32_t G0 = G;
+  C = 4;
+  if (!TBG_L0_SHAPE || G0 < 8 || rounds(G0, 4) <= 1) return;
+  double best = 0;
+  for (uint32_t k = 0; k < (g_free ? 3u : 2u); ++k) {
+    const double cost = (double)rounds(cand[k][0], cand[k][1]) * (0.948 + 1.395 * cand[k][1]);
+    if (best == 0 || cost < best) {
+      best = cost;
+      G = cand[k][0];
+      C = cand[k][1];
+    }
+  }
+}
+
 int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches, tbg_ticket* tickets) {
   if (!c || !bs || !tickets || n_batches == 0) return TBG_E_INVALID_ARG;
   int rc;
@@ -595,23 +630,15 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_hl = sec(4ull * LINES_WORDS * nm);
   if (c->rlc_auto)
     c->rlc_group = c->invalid_ema < TBG_RLC_AUTO_TO8 ? 16 : c->invalid_ema < TBG_RLC_AUTO_TO4 ? 8 : 4;
-  const uint32_t G = verify ? c->rlc_group : 0;
-  const uint32_t ng = G ? (nd + G - 1) / G : 0;
+  uint32_t G = verify ? c->rlc_group : 0;
   // Level 0 while the collected batches are clean (or as configured): one
   // failed level-0 check costs its own work on top of the group levels.
   const bool l0 = G != 0 && np < (1u << 28) &&
                   (c->rlc_batch == TBG_RLC_L0_ON || (c->rlc_batch == TBG_RLC_L0_AUTO && c->invalid_ema < TBG_RLC_AUTO_L0));
-  // Duties per Miller hexad: 4, or 8 for a level-0 launch of at least
-  // TBG_CHUNK8_DUTIES duties (unless tbg_config.rlc_chunk fixes it).  The
-  // level-0 Miller kernel's waves are long (the whole 68-step loop, ~6 ms),
-  // so a launch whose waves fill 1.5 rounds of the 2,048 two-wave slots
-  // runs two: config 4's 125k-DV shard at C = 4 is 3,126 waves (frac 0.49
-  // against 0.61 for the 160k-DV headline launch's 4,001, VERDICT r04 item
-  // 4).  At C = 8 a launch of n duties is ~n / 80 waves with half the
-  // squarings per duty: one round from ~120k duties on.
-  uint32_t Cw = c->rlc_chunk;
-  if (c->chunk_auto && l0 && nd >= TBG_CHUNK8_DUTIES) Cw = 8;
-  const uint32_t C = Cw < G ? Cw : (G ? G : 1);
+  uint32_t C = c->rlc_chunk;
+  if (l0 && c->chunk_auto) l0_shape(nd, c->hex_slots, c->rlc_auto && G == 16, G, C);
+  if (C > G) C = G ? G : 1;
+  const uint32_t ng = G ? (nd + G - 1) / G : 0;
   const uint32_t nch = G ? (G + C - 1) / C : 0;
   size_t w_pp = sec(G ? sizeof(G1J) * (size_t)np : 0);
   size_t w_ps = sec(G ? sizeof(G2J) * (size_t)np : 0);
@@ -1153,6 +1180,19 @@ int tbg_fetch_fallback(tbg_ctx* c, tbg_ticket t, uint32_t* out8) {
   out8[7] = s->op == TBG_OP_AGGREGATE || !s->B.rlc_batch ? (uint32_t)TBG_L0_NOT_RUN
             : cnt[CNT_L0_OK]                              ? (uint32_t)TBG_L0_PASSED
                                                           : (uint32_t)TBG_L0_FAILED;
+  return TBG_OK;
+}
+
+int tbg_fetch_shape(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
+  if (!c || !out4) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Slot* s = find_ticket(c, t, false, nullptr);
+  if (!s) return TBG_E_TICKET;
+  const uint32_t G = s->B.rlc_group, C = s->B.rlc_chunk;
+  out4[0] = G;
+  out4[1] = G ? C : 0;
+  out4[2] = s->B.rlc_batch ? 1u : 0u;
+  out4[3] = G ? ((s->n_duties + G - 1) / G) * ((G + C - 1) / C) : 0;
   return TBG_OK;
 }
 

@@ -13,10 +13,12 @@ namespace tbg {
 constexpr int kBlock = 64;
 // Default list positions per pass of the fallback levels' shared line buffer
 // (22.8 KB each: 0.75 GB per slot; tbg_config.fb_window overrides it).
-// Level-0 launches of at least this many duties run 8 duties per Miller
-// hexad instead of 4 (tbls_engine.hip, tbg_submit_group); 0xFFFFFFFF: never.
-#ifndef TBG_CHUNK8_DUTIES
-#define TBG_CHUNK8_DUTIES 120000u
+// Level-0 launch shape: a launch whose Miller hexads at (G, C) = (16, 4)
+// need more than one round of the device's wave slots picks (G, C) among
+// (16, 4), (16, 8), (14, 7) by rounds x hexad length (tbls_engine.hip,
+// l0_shape); 0: always (16, 4).
+#ifndef TBG_L0_SHAPE
+#define TBG_L0_SHAPE 1
 #endif
 #ifndef TBG_FB_WINDOW
 #define TBG_FB_WINDOW 32768u

@@ -240,6 +240,13 @@ class Engine:
         return dict(zip(["groups", "group_searches", "chunks", "chunk_searches", "duty_searches", "partial_checks",
                          "group_size", "level0"], out.tolist()))
 
+    def shape(self, ticket) -> dict:
+        """Verification shape of the batch's last submit (tbg_fetch_shape):
+        duties per group and per Miller chunk, level 0, P-chunk hexads."""
+        out = np.zeros(4, dtype=np.uint32)
+        self._check(self._lib.tbg_fetch_shape(self._h, ticket, _ptr(out)), "tbg_fetch_shape")
+        return dict(zip(["group", "chunk", "level0", "chunks"], out.tolist()))
+
     def subgroup(self, ticket) -> dict:
         """Batched subgroup test of the batch's last run (tbg_fetch_subgroup):
         groups of 512 partials tested by random combinations (0: every

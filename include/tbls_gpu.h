@@ -260,6 +260,11 @@ int tbg_fetch_fallback(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out8);
  * combinations (0: every signature was tested alone), groups that failed
  * (their members were then tested one by one)]. */
 int tbg_fetch_subgroup(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out2);
+/* Verification shape of a collected batch's last submit: out4 = [duties per
+ * group G, duties per Miller chunk C, level 0 on (1) or off, Miller P-chunk
+ * hexads G x C cut the batch into].  A level-0 launch with neither G nor C
+ * configured picks (G, C) by the device's wave slots. */
+int tbg_fetch_shape(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out4);
 /* Host-side work of the context's submit / collect calls since the last
  * reset (reset != 0 zeroes the counters after reading): out8 = [submit
  * calls, partials submitted, ns packing the callers' arrays into pinned

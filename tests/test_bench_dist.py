@@ -61,8 +61,12 @@ def test_roofline_fields_from_work_model():
     wm = bench.work_model()
     assert wm is not None and "kernels" in wm
     b = types.SimpleNamespace(n_dv=10000, identifiers=np.zeros(40000), msg_off=np.zeros(10001))
-    items = bench.launch_items([b] * 16, 16)
-    assert items == {"partial": 640000, "message": 160000, "duty": 160000, "group": 10000, "launch": 1}
+    items = bench.launch_items([b] * 16, {"group": 16, "chunk": 4, "level0": 1, "chunks": 40000})
+    assert items == {"partial": 640000, "message": 160000, "duty": 160000, "group": 10000, "chunk": 40000,
+                     "launch": 1}
+    # the level-0 launch shape (16, 8): half the P chunks, same duties
+    items8 = bench.launch_items([b] * 16, {"group": 16, "chunk": 8, "level0": 1, "chunks": 20000})
+    assert items8["chunk"] == 20000 and items8["group"] == 10000
     prof = [("k_decode_sigs", 9.0), ("k_subgroup_sigs", 13.4), ("k_miller_hex<MILLER_L0>", 15.9),
             ("k_miller_hex<MILLER_GROUP_S>", 0.005), ("k_msm_sum", 0.4), ("k_msm_sum", 0.1)]
     kp = bench.kernel_profile(prof)
@@ -73,7 +77,9 @@ def test_roofline_fields_from_work_model():
                                                                      "WRITE_SIZE_KB_per_launch": 10.0}}}
     r = bench.kernel_roofline(wm, kp, items, tm, 16)
     m = wm["kernels"]["k_miller_hex<MILLER_L0>"]
-    mads = m["mads"] * 10000 + m["plus_per_launch"]
+    mads = m["mads"] * 40000 + m["plus"]["duty"] * 160000 + m["plus_per_launch"]
+    # the per-chunk + per-duty form equals count_work's measured 4-duty chunk
+    assert abs(4 * m["plus"]["duty"] + m["mads"] - wm["mads"]["rlc_miller_chunk"]) <= 4
     assert r["kernel"] == "k_miller_hex<MILLER_L0>" == r["dominant_by_exclusive_time"]
     assert r["rocprof_name"] == "void tbg::k_miller_hex<1>(tbg::DevBatch)"
     assert r["traffic"] == 1024 * 210
@@ -89,6 +95,10 @@ def test_roofline_fields_from_work_model():
     assert r2["dominant_by_exclusive_time"] == "k_mystery" and r2["kernel"] == "k_miller_hex<MILLER_L0>"
     pipe = bench.pipeline_roofline(wm, 1.0e6, True, 3, 4)
     assert abs(pipe["achieved"] - 1.0e6 * wm["mads"]["unit_3of4_l0"] / 1e12) < 1e-2
+    assert bench.pipeline_roofline(wm, 1.0e6, True, 3, 4, items=items)["achieved"] == pipe["achieved"]
+    # 8-duty chunks: fewer squarings per duty, less algorithmic work per unit
+    pipe8 = bench.pipeline_roofline(wm, 1.0e6, True, 3, 4, items=items8)
+    assert pipe8["work_per_unit_mads"] < pipe["work_per_unit_mads"]
     assert 0 < pipe["frac"] < 1
     assert bench.pipeline_roofline(wm, 1.0e6, True, 7, 10) is None
 

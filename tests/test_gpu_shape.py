@@ -1,0 +1,90 @@
+"""The level-0 launch shape (tbls_engine.hip l0_shape):
+a level-0 launch whose Miller hexads at (G, C) = (16, 4) need more than one
+round of the device's wave slots takes the (G, C) with the fewest rounds x
+hexad length.  Config 4's 125k-DV shard runs at (14, 7) on MI355X, and its
+verdicts -- level 0 passing, and one wrong-share partial found through the
+G = 14 group levels -- equal the known answers and oracle/c on a 10k slice."""
+import numpy as np
+import pytest
+
+from tests.conftest import progress
+from tests.test_gpu_fullsize import assert_same, oracle_run
+from tests.test_gpu_headline import _call, _known_answer
+
+pytestmark = pytest.mark.gpu
+DVS = 125000
+
+
+def expected_shape(nd, n_cu, g_free=True, G=16):
+    """Mirror of l0_shape: rounds of (CUs x 4 SIMDs x 2) hexad waves x the
+    hexad cost 0.948 + 1.395 C (M u32 mul-adds, profiles/work_model.json)."""
+    slots = n_cu * 8
+
+    def rounds(g, c):
+        hexads = -(-nd // g) * -(-g // c)
+        return -(-(-(-hexads // 10)) // slots)
+
+    if rounds(G, 4) <= 1:
+        return G, 4
+    cand = [(16 if g_free else G, 4), (16 if g_free else G, 8)] + ([(14, 7)] if g_free else [])
+    return min(cand, key=lambda gc: (rounds(*gc) * (0.948 + 1.395 * gc[1]), cand.index(gc)))
+
+
+def test_shape_mirror():
+    assert expected_shape(160000, 256) == (16, 8)
+    assert expected_shape(125000, 256) == (14, 7)
+    assert expected_shape(10000, 256) == (16, 4)
+    assert expected_shape(125000, 256, g_free=False, G=16) == (16, 8)
+
+
+@pytest.fixture(scope="module")
+def shard():
+    from charon_amd import engine as eng
+    from tools.workload import make_batch
+    e = eng.Engine(0, slots=1)  # group size and chunk not configured: the engine picks them
+    b = make_batch(e, DVS, 3, 4, seed=4125)
+    yield e, b
+    e.close()
+
+
+def _submit(e, b):
+    from charon_amd import engine as eng
+    t = e.submit(eng.OP_VERIFY_AGGREGATE, **_call(b))
+    return t, e.collect(t)
+
+
+def test_config4_shard_shape_level0_passes(shard):
+    import torch
+    from charon_amd import engine as eng
+    e, b = shard
+    t, res = _submit(e, b)
+    G, C = expected_shape(DVS, torch.cuda.get_device_properties(0).multi_processor_count)
+    sh = e.shape(t)
+    progress(f"shape {sh}")
+    assert (sh["group"], sh["chunk"], sh["level0"]) == (G, C, 1)
+    assert sh["chunks"] == -(-DVS // G) * -(-G // C)
+    assert e.level0(t) == eng.L0_PASSED
+    _known_answer(res, b)
+    s0 = 60000
+    assert_same(res, oracle_run(b, s0, s0 + 10000), s0, s0 + 10000, int(b.duty_first[s0]))
+
+
+def test_config4_shard_shape_one_invalid_partial(shard):
+    from dataclasses import replace
+    from charon_amd import engine as eng
+    e, b = shard
+    rng = np.random.default_rng(125)
+    i = int(rng.integers(0, len(b.identifiers)))
+    d = i // 4
+    sigs = b.sigs.copy()
+    sigs[i] = b.sigs[4 * d + (i - 4 * d + 1) % 4]  # wrong share
+    injected = b.injected.copy()
+    injected[i] = True
+    bad = replace(b, sigs=sigs, injected=injected, expect_ok=b.expect_ok.copy())
+    t, res = _submit(e, bad)
+    assert e.level0(t) == eng.L0_FAILED
+    assert e.shape(t)["chunk"] > 4  # the group levels ran on the wide launch shape
+    assert np.flatnonzero(res.partial_status != eng.PS_VALID).tolist() == [i]
+    _known_answer(res, bad)
+    s0 = max(0, min(d - 5000, DVS - 10000))
+    assert_same(res, oracle_run(bad, s0, s0 + 10000), s0, s0 + 10000, int(bad.duty_first[s0]))

@@ -94,6 +94,13 @@ def main():
     qmul = measure(lib.hc_stage_group_final, 2)[0] - final1
     s_quad, _ = measure(lib.hc_stage_miller_chunk, 0, 1)
     nch = G // C
+    # a P-chunk hexad of c duties costs base + c * per_duty (62 squarings, 68
+    # line products per duty): the level-0 launch shape (G, C) varies with the
+    # launch size (tbls_engine.hip l0_shape), so the kernels' models are per
+    # chunk and per duty
+    chunk8, _ = measure(lib.hc_stage_miller_chunk, 8, 0)
+    chunk_per_duty = (chunk8 - chunk2) / 4
+    chunk_base = chunk2 - 4 * chunk_per_duty
     # per-kernel probes (one item of each kernel of the level-0 chain)
     for fn in ("hc_k_decode_sigs", "hc_k_subgroup_sigs"):
         getattr(lib, fn).restype = ctypes.c_int
@@ -169,6 +176,7 @@ def main():
                  "l0_partial": l0_partial, "l0_duty_sum_4": duty_sum_p4, "l0_per_group": l0_per_group,
                  "l0_per_launch": round(l0_per_launch), "l0_bucket_scales": round(bucket_scales),
                  "g2_add": g2_add, "quad_mul": qmul, "l0_s_quad": s_quad, "final_exp_quad": final1,
+                 "l0_chunk_base": round(chunk_base), "l0_chunk_per_duty": round(chunk_per_duty),
                  "unit_3of4_l0": round(unit_3of4_l0), "l0_launch_dvs": launch_dvs,
                  "unit_3of4_l0_subgroup_alone": round(unit_3of4_l0_alone),
                  "decode_sig_batched_subgroup": round(decode_sgb), "sgb_per_partial": round(sgb_per_partial),
@@ -206,8 +214,9 @@ def main():
             "k_msm_bucket": {"per": "launch", "mads": round(bucket_scales + 32768 * (4 - 1) * g2_add)},
             "k_rlc_duty_sum<DSUM_L0_P>": {"per": "duty", "mads": round(duty_sum_p4)},
             # the level-0 P-chunk products on hexads (bls_hex.h) + the one S hexad
-            "k_miller_hex<MILLER_L0>": {"per": "group", "mads": round(nch * chunk2), "plus_per_launch": s_quad},
-            "k_l0_fold": {"per": "group", "mads": round((nch - 1) * qmul)},
+            "k_miller_hex<MILLER_L0>": {"per": "chunk", "mads": round(chunk_base), "plus": {"duty": round(chunk_per_duty)},
+                                        "plus_per_launch": s_quad},
+            "k_l0_fold": {"per": "chunk", "mads": round(qmul), "plus": {"group": -round(qmul)}},
             "k_l0_final": {"per": "launch", "mads": round(final1)},
             "k_aggregate<true>": {"per": "duty", "mads": round(agg)},
             "k_aggregate<false>": {"per": "duty", "mads": round(agg)},
