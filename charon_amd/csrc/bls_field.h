@@ -478,52 +478,6 @@ TBG_NI Fp fp_pow_const(const Fp& a) {
   return r;
 }
 
-// Two exponentiations by the same fixed exponent, interleaved: one window
-// scan drives both, so every squaring / product of a comes with an
-// independent one of b and the scheduler fills one chain's carry-chain
-// latency with the other's multiply-adds (k_hash_map's two SSWU maps).
-// Width 3: the two 4-entry tables fit where one 8-entry table did.
-struct FpPair { Fp a, b; };
-template <int NBITS, const uint32_t (&WD)[12]>
-TBG_NI FpPair fp_pow_const_x2(const Fp& a, const Fp& b) {
-  const Fp a2 = fp_sqr(a), b2 = fp_sqr(b);
-  const Fp a3 = fp_mul(a, a2), b3 = fp_mul(b, b2);
-  const Fp a5 = fp_mul(a3, a2), b5 = fp_mul(b3, b2);
-  const Fp a7 = fp_mul(a5, a2), b7 = fp_mul(b5, b2);
-  auto bit = [&](int i) -> uint32_t { return (WD[i >> 5] >> (i & 31)) & 1u; };
-  Fp r = a, s = b;
-  bool started = false;
-  int i = NBITS - 1;  // top bit is 1
-  while (i >= 0) {
-    if (!bit(i)) {
-      r = fp_sqr(r);
-      s = fp_sqr(s);
-      --i;
-      continue;
-    }
-    int L = i + 1 < 3 ? i + 1 : 3;
-    while (!bit(i - L + 1)) --L;
-    uint32_t v = 0;
-    for (int k = 0; k < L; ++k) v = (v << 1) | bit(i - k);
-    const Fp ta = fp_select(v == 1, a, fp_select(v == 3, a3, fp_select(v == 5, a5, a7)));
-    const Fp tb = fp_select(v == 1, b, fp_select(v == 3, b3, fp_select(v == 5, b5, b7)));
-    if (started) {
-      for (int k = 0; k < L; ++k) {
-        r = fp_sqr(r);
-        s = fp_sqr(s);
-      }
-      r = fp_mul(r, ta);
-      s = fp_mul(s, tb);
-    } else {
-      r = ta;
-      s = tb;
-      started = true;
-    }
-    i -= L;
-  }
-  return {r, s};
-}
-
 // Fermat: a^(p-2), ~380 squarings + ~95 products in one dependent chain
 // (0.44 ms on a lone lane, profiles/r03/wide_fe.txt).
 TBG_HD Fp fp_inv_fermat(const Fp& a) { return fp_pow_const<EXP_INV_BITS, EXP_INV_WORDS>(a); }

@@ -373,42 +373,6 @@ TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) {
   return fp2_eq(fp2_sqr(r), a);
 }
 
-// fp2_sqrt_or_z of both maps' g(x1) at once: the two norms' and the two
-// deltas' exponentiations interleaved (fp_pow_const_x2).  Returns bit j set
-// when root j is valid (the closed form covers input j), bit 2 + j when
-// a_j itself is the square.
-TBG_NI uint32_t fp2_sqrt_or_z_x2(const Fp2& a0_in, const Fp2& a1_in, Fp2& r0, Fp2& r1) {
-  Fp2 a[2] = {fp2_reduce(a0_in), fp2_reduce(a1_in)};
-  Fp norm[2];
-  for (int j = 0; j < 2; ++j) norm[j] = fp_mul2(a[j].c0, a[j].c0, a[j].c1, a[j].c1);
-  const FpPair g = fp_pow_const_x2<EXP_SQRT_BITS, EXP_SQRT_WORDS>(norm[0], norm[1]);
-  Fp gamma[2] = {g.a, g.b}, delta[2];
-  const Fp inv2 = fp_from_const(INV2_M);
-  uint32_t flags = 0;
-  for (int j = 0; j < 2; ++j) {
-    const bool sq = fp_eq(fp_sqr(gamma[j]), norm[j]);
-    if (!sq) {
-      // gamma^2 = -norm(a); K gamma is a root of norm(Z) norm(a) = norm(Z a)
-      a[j] = fp2_reduce(fp2_mul(fp2_from_const(SSWU_Z), a[j]));
-      gamma[j] = fp_mul(gamma[j], fp_from_const(SSWU_SQRT_NEG_NORM_Z));
-    }
-    flags |= sq ? 4u << j : 0u;
-    delta[j] = fp_mul(fp_add(a[j].c0, gamma[j]), inv2);
-  }
-  const FpPair t = fp_pow_const_x2<EXP_PM3D4_BITS, EXP_PM3D4_WORDS>(delta[0], delta[1]);  // delta^((p-3)/4)
-  Fp2* out[2] = {&r0, &r1};
-  for (int j = 0; j < 2; ++j) {
-    const Fp tj = j ? t.b : t.a;
-    const Fp x0 = fp_mul(delta[j], tj);
-    const Fp h = fp_mul(fp_mul(a[j].c1, tj), inv2);
-    const bool res = fp_eq(fp_sqr(x0), delta[j]);
-    const Fp2 r = {fp_select(res, x0, h), fp_select(res, h, fp_reduce(fp_neg(x0)))};
-    *out[j] = r;
-    if (!fp_is_zero(a[j].c1) && fp2_eq(fp2_sqr(r), a[j])) flags |= 1u << j;
-  }
-  return flags;
-}
-
 // SSWU of both hash_to_field outputs with uniform control flow: one Fp2
 // inversion for the two denominators (Montgomery's trick) and one square
 // root per map -- when g(x1) is not a square, x2 = Z u^2 x1 and
@@ -434,19 +398,19 @@ TBG_NI void sswu_pair_finish(const Fp2& u0, const Fp2& u1, const SswuPair& w, bo
                              G2J& q1) {
   const Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B), Z = fp2_from_const(SSWU_Z);
   const Fp2* u[2] = {&u0, &u1};
-  const Fp2 inv[2] = {fp2_mul(w.den[1], di), fp2_mul(w.den[0], di)};
+  Fp2 inv[2] = {fp2_mul(w.den[1], di), fp2_mul(w.den[0], di)};
   G2J* out[2] = {&q0, &q1};
-  Fp2 x1[2], gx1[2], r[2];
-  for (int j = 0; j < 2; ++j) {
-    x1[j] = fp2_mul(fp2_from_const(SSWU_NEG_B_OVER_A), fp2_reduce(fp2_add(fp2_one(), inv[j])));
-    gx1[j] = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_sqr(x1[j]), x1[j]), fp2_mul(A, x1[j])), B));
-  }
-  const uint32_t f = ok ? fp2_sqrt_or_z_x2(gx1[0], gx1[1], r[0], r[1]) : 0u;
-  ok = ok && (f & 3u) == 3u;
   for (int j = 0; j < 2 && ok; ++j) {
-    const bool sq = (f >> (2 + j)) & 1u;
-    Fp2 x = sq ? x1[j] : fp2_mul(w.zu2[j], x1[j]);
-    Fp2 y = sq ? r[j] : fp2_mul(fp2_mul(Z, fp2_mul(fp2_sqr(*u[j]), *u[j])), r[j]);
+    Fp2 x1 = fp2_mul(fp2_from_const(SSWU_NEG_B_OVER_A), fp2_reduce(fp2_add(fp2_one(), inv[j])));
+    Fp2 gx1 = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_sqr(x1), x1), fp2_mul(A, x1)), B));
+    Fp2 r;
+    bool sq;
+    if (!fp2_sqrt_or_z(gx1, r, sq)) {
+      ok = false;
+      break;
+    }
+    Fp2 x = sq ? x1 : fp2_mul(w.zu2[j], x1);
+    Fp2 y = sq ? r : fp2_mul(fp2_mul(Z, fp2_mul(fp2_sqr(*u[j]), *u[j])), r);
     if (fp2_sgn0(*u[j]) != fp2_sgn0(y)) y = fp2_reduce(fp2_neg(y));
     *out[j] = iso3_to_jac(x, y);
   }

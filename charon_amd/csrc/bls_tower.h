@@ -105,40 +105,6 @@ TBG_NI bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
   return true;
 }
 
-// Square roots of two Fp2 values at once (k_decode_sigs, two signatures per
-// lane): the norms' and the deltas' exponentiations interleaved
-// (fp_pow_const_x2).  Bit j of the result: out_j is a root of a_j; bit 2 + j:
-// a_j lies in Fp (a_j.c1 == 0), which this closed form does not cover --
-// the caller runs fp2_sqrt on it.
-TBG_NI uint32_t fp2_sqrt_x2(const Fp2& a0_in, const Fp2& a1_in, Fp2& out0, Fp2& out1) {
-  const Fp2 a[2] = {fp2_reduce(a0_in), fp2_reduce(a1_in)};
-  Fp norm[2];
-  for (int j = 0; j < 2; ++j) norm[j] = fp_mul2(a[j].c0, a[j].c0, a[j].c1, a[j].c1);
-  const FpPair g = fp_pow_const_x2<EXP_SQRT_BITS, EXP_SQRT_WORDS>(norm[0], norm[1]);
-  const Fp gamma[2] = {g.a, g.b};
-  const Fp inv2 = fp_from_const(INV2_M);
-  Fp delta[2];
-  uint32_t flags = 0, nsq = 0;
-  for (int j = 0; j < 2; ++j) {
-    if (fp_is_zero(a[j].c1)) flags |= 4u << j;
-    if (!fp_eq(fp_sqr(gamma[j]), norm[j])) nsq |= 1u << j;  // norm not a square: a_j is not
-    delta[j] = fp_mul(fp_add(a[j].c0, gamma[j]), inv2);
-  }
-  const FpPair t = fp_pow_const_x2<EXP_PM3D4_BITS, EXP_PM3D4_WORDS>(delta[0], delta[1]);  // delta^((p-3)/4)
-  Fp2* out[2] = {&out0, &out1};
-  for (int j = 0; j < 2; ++j) {
-    const Fp tj = j ? t.b : t.a;
-    const Fp x0 = fp_mul(delta[j], tj);
-    const Fp h = fp_mul(fp_mul(a[j].c1, tj), inv2);
-    const bool res = fp_eq(fp_sqr(x0), delta[j]);
-    // residue: (sqrt(delta), a1 / (2 x0)); otherwise (a1 t / 2, -delta t)
-    const Fp2 r = {fp_select(res, x0, h), fp_select(res, h, fp_reduce(fp_neg(x0)))};
-    *out[j] = r;
-    if (!((nsq | (flags >> 2)) >> j & 1u) && fp2_eq(fp2_sqr(r), a[j])) flags |= 1u << j;
-  }
-  return flags;
-}
-
 // Legendre-style square test in Fp2: a is a square iff norm(a) is a square in Fp.
 TBG_NI bool fp2_is_square(const Fp2& a) {
   Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);

@@ -45,11 +45,31 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_decode_pubkeys(const uint8_t* pk
 
 // Decode in two kernels so each runs at the occupancy its own register
 // footprint allows (one kernel would take the maximum of both):
-//   k_decode_sigs    flags, field, Fp2 square root (Fp exponentiations;
-//                    k_decode_sig.hip: a translation unit without
-//                    TBG_SCHED_FENCE, two signatures per lane);
+//   k_decode_sigs    one lane per signature: flags, field, Fp2 square root
+//                    (Fp exponentiations: small state, several waves per SIMD);
 //   k_subgroup_sigs  one lane PAIR per decoded signature: psi(a) == [x] a with
 //                    the Fp2 coordinates split over the pair (bls_pair.h).
+__global__ void TBG_LAUNCH_N(TBG_DECODE_WAVES) k_decode_sigs(DevBatch B) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // The chain's first kernel zeroes its work-list counters and level 0's
+  // bucket sizes (a runtime memset kernel queued behind other streams' waves
+  // held each chain for ~2 ms in the pipelined bench)
+  if (i < CNT_WORDS) B.counters[i] = 0;
+  if (B.rlc_batch && i <= MSM_BUCKETS) B.msm_off[i] = 0;
+  if (i >= B.n_partials) return;
+  uint8_t b[96];
+  for (int j = 0; j < 96; ++j) b[j] = B.sigs[96ull * i + j];
+  G2A a;
+  int32_t st = g2_decompress_t<true, false>(b, a);
+  if (st == DEC_IDENTITY) st = TBG_PS_ERR_IDENTITY;
+  if (st != DEC_OK) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+  }
+  B.sig_aff[i] = a;
+  B.partial_status[i] = (st == DEC_OK) ? TBG_PS_NOT_VERIFIED : st;
+}
+
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_subgroup_sigs(DevBatch B) {
   const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (i >= B.n_partials) return;
@@ -76,7 +96,9 @@ void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x
 }
 void launch_decode_sigs(const DevBatch& B, hipStream_t st) {
   // at least enough lanes to zero the counters (and level 0's bucket sizes)
-  launch_decode_roots(B, st);  // k_decode_sig.hip
+  uint32_t lanes = B.n_partials > CNT_WORDS ? B.n_partials : CNT_WORDS;
+  if (B.rlc_batch && lanes < MSM_BUCKETS + 1) lanes = MSM_BUCKETS + 1;
+  TBG_KLAUNCH(k_decode_sigs, grid_for(lanes), dim3(kBlock), st, B);
   launch_subgroup_batch(B, st);
   if (B.n_partials) TBG_KLAUNCH(k_subgroup_sigs, grid_for(2 * B.n_partials), dim3(kBlock), st, B);
 }

@@ -535,29 +535,34 @@ static Slot* find_ticket(tbg_ctx* c, tbg_ticket t, bool want_pending, Part** par
 int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) { return tbg_submit_group(c, &b, 1, ticket); }
 
 // Level-0 launch shape.  The level-0 Miller kernel's
-// waves are long (one hexad = the whole 68-step loop over C duties, ~6 ms)
-// and all alike, so a launch takes ceil(waves / slots) rounds of one hexad's
-// time: config 4's 125k-duty shard at (16, 4) is 3,126 waves, 1.53 rounds
-// of 2,048 two-wave slots, run as two.  A hexad of C duties costs 62
-// squarings + 68 C line products, 0.95 M + 1.39 M C u32 mul-adds
-// (profiles/work_model.json, l0_chunk_*), so fewer, longer hexads win where
-// they save a round:
-// (16, 8) halves the squarings and runs 160k duties in one round, (14, 7)
-// runs 125k in 0.87 of one.  Launches within one round at (16, 4) keep it;
-// a configured group size G keeps G (C = 4 or 8 only).
+// waves are long (one hexad = the whole 68-step loop over C duties, ~6 ms
+// at C = 4) and all alike, so its time is set by rounds of the device's
+// two-wave slots: config 4's 125k-duty shard at (G, C) = (16, 4) is 3,126
+// waves, 1.53 rounds of 2,048 slots.  A hexad of C duties costs 62
+// squarings + 68 C line products, w(C) = 0.95 M + 1.39 M C u32 mul-adds
+// (profiles/work_model.json, l0_chunk_*), so fewer, longer hexads win
+// where they save a round: (16, 8) halves the squarings, (14, 7) runs 125k
+// duties in 0.87 of a round.  The kernel's time is modelled as w(C) x
+// (whole rounds + min(1, 0.25 + 1.25 x the last round's fill)): a partly
+// filled last round runs its waves with the SIMDs to themselves (fitted to
+// the six A/B points of profiles/r05/chunk8_ab, shape_ab, sqrt_x2_ab within
+// 4 %: 100k duties keep (16, 4), 125k take (14, 7), 160k (16, 8)).  A
+// configured group size G keeps G (C = 4 or 8 only).
+static double l0_shape_cost(uint32_t nd, uint32_t slots, uint32_t g, uint32_t ch) {
+  const uint64_t hexads = (uint64_t)((nd + g - 1) / g) * ((g + ch - 1) / ch);
+  const double r = (double)((hexads + 9) / 10) / (double)slots;
+  const double whole = (double)(uint64_t)r, part = r - whole;
+  return (0.948 + 1.395 * ch) * (whole + (part > 0 ? std::min(1.0, 0.25 + 1.25 * part) : 0.0));
+}
 static void l0_shape(uint32_t nd, uint32_t slots, bool g_free, uint32_t& G, uint32_t& C) {
   const uint32_t cand[3][2] = {{g_free ? 16u : G, 4}, {g_free ? 16u : G, 8}, {14, 7}};
-  auto rounds = [&](uint32_t g, uint32_t ch) {
-    const uint64_t hexads = (uint64_t)((nd + g - 1) / g) * ((g + ch - 1) / ch);
-    return ((hexads + 9) / 10 + slots - 1) / slots;
-  };
-  const uint32_t G0 = G;
   C = 4;
-  if (!TBG_L0_SHAPE || G0 < 8 || rounds(G0, 4) <= 1) return;
-  double best = 0;
-  for (uint32_t k = 0; k < (g_free ? 3u : 2u); ++k) {
-    const double cost = (double)rounds(cand[k][0], cand[k][1]) * (0.948 + 1.395 * cand[k][1]);
-    if (best == 0 || cost < best) {
+  if (!TBG_L0_SHAPE || G < 8) return;
+  const uint32_t G0 = G;
+  double best = l0_shape_cost(nd, slots, G0, 4);
+  for (uint32_t k = 1; k < (g_free ? 3u : 2u); ++k) {
+    const double cost = l0_shape_cost(nd, slots, cand[k][0], cand[k][1]);
+    if (cost < best) {
       best = cost;
       G = cand[k][0];
       C = cand[k][1];

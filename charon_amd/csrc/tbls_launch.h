@@ -264,7 +264,6 @@ void launch_sum_g2(const uint8_t* sigs96, const SumPlan& p, uint8_t* out96, int3
 void launch_decode_pubkeys(const uint8_t* pk48, uint32_t n, G1A* out, G1A* out_x, int32_t* status, hipStream_t st);
 void launch_decode_sigs(const DevBatch& B, hipStream_t st);
 // the batched subgroup test (B.sgb): sort, bucket sums, combination checks
-void launch_decode_roots(const DevBatch& B, hipStream_t st);
 void launch_subgroup_batch(const DevBatch& B, hipStream_t st);
 void launch_hash_msgs(const DevBatch& B, hipStream_t st);
 void launch_hash_clear(const DevBatch& B, hipStream_t st);

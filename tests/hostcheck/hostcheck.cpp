@@ -50,17 +50,6 @@ int hc_fp2_sqrt(const uint8_t* a, uint8_t* out) {
   return 1;
 }
 
-// fp2_sqrt_x2 on (a, b): returns its flags, roots into out (a's, then b's)
-uint32_t hc_fp2_sqrt_x2(const uint8_t* a, const uint8_t* b, uint8_t* out) {
-  Fp2 x = {from_be(a), from_be(a + 48)}, y = {from_be(b), from_be(b + 48)}, r0, r1;
-  const uint32_t f = fp2_sqrt_x2(x, y, r0, r1);
-  to_be(r0.c0, out);
-  to_be(r0.c1, out + 48);
-  to_be(r1.c0, out + 96);
-  to_be(r1.c1, out + 144);
-  return f;
-}
-
 // Fp12 multiply/square/inverse/frobenius on 12 Fp2 coefficient in order
 // c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2 (each c0 || c1, 96 bytes).
 static Fp12 f12_in(const uint8_t* b) {

@@ -16,24 +16,32 @@ DVS = 125000
 
 
 def expected_shape(nd, n_cu, g_free=True, G=16):
-    """Mirror of l0_shape: rounds of (CUs x 4 SIMDs x 2) hexad waves x the
-    hexad cost 0.948 + 1.395 C (M u32 mul-adds, profiles/work_model.json)."""
+    """Mirror of l0_shape: the hexad cost 0.948 + 1.395 C (M u32 mul-adds,
+    profiles/work_model.json) x (whole rounds of the CUs x 4 SIMDs x 2 wave
+    slots + min(1, 0.25 + 1.25 x the last round's fill))."""
     slots = n_cu * 8
 
-    def rounds(g, c):
-        hexads = -(-nd // g) * -(-g // c)
-        return -(-(-(-hexads // 10)) // slots)
+    def cost(g, c):
+        r = -(-(-(-nd // g) * -(-g // c)) // 10) / slots
+        whole = int(r)
+        part = r - whole
+        return (0.948 + 1.395 * c) * (whole + (min(1.0, 0.25 + 1.25 * part) if part > 0 else 0.0))
 
-    if rounds(G, 4) <= 1:
+    if G < 8:
         return G, 4
     cand = [(16 if g_free else G, 4), (16 if g_free else G, 8)] + ([(14, 7)] if g_free else [])
-    return min(cand, key=lambda gc: (rounds(*gc) * (0.948 + 1.395 * gc[1]), cand.index(gc)))
+    best = cand[0]
+    for gc in cand[1:]:
+        if cost(*gc) < cost(*best):
+            best = gc
+    return best
 
 
 def test_shape_mirror():
     assert expected_shape(160000, 256) == (16, 8)
     assert expected_shape(125000, 256) == (14, 7)
     assert expected_shape(10000, 256) == (16, 4)
+    assert expected_shape(100000, 256) == (16, 4)  # config 3's launch (1.22 rounds at C = 4)
     assert expected_shape(125000, 256, g_free=False, G=16) == (16, 8)
 
 

@@ -96,34 +96,6 @@ def test_fp2_mul_and_sqrt():
         assert bls.f2_sqr(b2f(ob.raw)) == (a0, 0)
 
 
-
-def test_fp2_sqrt_x2_pairs():
-    """fp2_sqrt_x2 (k_decode_sigs: two signatures' square roots interleaved)
-    on pairs of squares, non-squares and Fp elements: bit j says whether root
-    j is valid, bit 2 + j flags the a_j.c1 == 0 case the caller hands to
-    fp2_sqrt; every valid root squares back."""
-    import ctypes
-    fn = lib().hc_fp2_sqrt_x2
-    fn.restype = ctypes.c_uint32
-    vals = []
-    for _ in range(6):
-        a = (rng.randrange(P), rng.randrange(P))
-        vals += [bls.f2_sqr(a), a]  # a square, and a random value (square half the time)
-    vals += [(5, 0), (0, 0), (P - 1, 0)]
-    for k in range(len(vals)):
-        a, b = vals[k], vals[(k * 7 + 3) % len(vals)]
-        ob = ctypes.create_string_buffer(192)
-        f = fn(f2b(a), f2b(b), ob)
-        for j, x in enumerate((a, b)):
-            in_fp = x[1] == 0
-            assert (f >> (2 + j)) & 1 == (1 if in_fp else 0)
-            if in_fp:
-                continue
-            ok = (f >> j) & 1
-            assert ok == (1 if bls.f2_is_square(x) else 0), (x, f)
-            if ok:
-                assert bls.f2_sqr(b2f(ob.raw[96 * j:96 * j + 96])) == x
-
 def f12b(f):
     (a, b, c), (d, e, g) = f
     return b"".join(f2b(x) for x in (a, b, c, d, e, g))

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch-partials", type=int, default=40000)
     ap.add_argument("--bin", type=float, default=0.5)
+    ap.add_argument("--per-lane", type=int, default=1, help="signatures per k_decode_sigs lane")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), grid(r),
@@ -52,7 +53,7 @@ def main():
         cur.append(e)
     if cur:
         groups.append(cur)
-    want = a.steps * a.batch_partials
+    want = a.steps * a.batch_partials // a.per_lane
     timed = None
     for g in groups:
         if abs(sum(x[3] for x in g) - want) <= 64 * len(g) * 16:
