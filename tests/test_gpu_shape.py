@@ -47,11 +47,13 @@ def test_shape_mirror():
 
 @pytest.fixture(scope="module")
 def shard():
+    import torch
     from charon_amd import engine as eng
     from tools.workload import make_batch
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count  # (before the engine's own HIP calls)
     e = eng.Engine(0, slots=1)  # group size and chunk not configured: the engine picks them
     b = make_batch(e, DVS, 3, 4, seed=4125)
-    yield e, b
+    yield e, b, n_cu
     e.close()
 
 
@@ -62,11 +64,10 @@ def _submit(e, b):
 
 
 def test_config4_shard_shape_level0_passes(shard):
-    import torch
     from charon_amd import engine as eng
-    e, b = shard
+    e, b, n_cu = shard
     t, res = _submit(e, b)
-    G, C = expected_shape(DVS, torch.cuda.get_device_properties(0).multi_processor_count)
+    G, C = expected_shape(DVS, n_cu)
     sh = e.shape(t)
     progress(f"shape {sh}")
     assert (sh["group"], sh["chunk"], sh["level0"]) == (G, C, 1)
@@ -80,7 +81,7 @@ def test_config4_shard_shape_level0_passes(shard):
 def test_config4_shard_shape_one_invalid_partial(shard):
     from dataclasses import replace
     from charon_amd import engine as eng
-    e, b = shard
+    e, b, _ = shard
     rng = np.random.default_rng(125)
     i = int(rng.integers(0, len(b.identifiers)))
     d = i // 4
