@@ -108,12 +108,28 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_bucket(DevBatch B, uint32_t n
   px_store(B.sgb_part[w], acc);
 }
 
-// one lane pair per (group, combination): Q_k = sum_v v B_v by running sums
-// from v = 6 down, stored over the combination's first slice (only this pair
-// reads those slices).  The additions skip the doubling case (bls_pair.h
+// one lane pair per (group, bucket): the bucket's SGB_SPLIT slice sums into
+// its first slice, so the running sums below are 2 x SGB_V additions deep
+// instead of (SGB_SPLIT + 1) x SGB_V (a latency-bound kernel: few waves,
+// each one serial chain).  The additions skip the doubling case (bls_pair.h
 // jac_add_x: fewer live values than the complete formulas): two equal
 // partial sums -- which random digits make negligible -- fail the group,
 // whose members are then tested one by one.
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_fold(DevBatch B, uint32_t n_sg) {
+  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
+  if (w >= n_sg * SGB_BUCKETS) return;
+  G2J* part = B.sgb_part + (size_t)w * SGB_SPLIT;
+  Jac<Fp2x> acc = px_load(part[0]);
+  bool exc = false;
+#pragma unroll 1
+  for (uint32_t sl = 1; sl < SGB_SPLIT; ++sl) acc = jac_add_x(acc, px_load(part[sl]), exc);
+  if (pair_all(!exc)) px_store(part[0], acc);
+  else if (pair_par() == 0) B.sgb_bad[w / SGB_BUCKETS] = 1u;
+}
+
+// one lane pair per (group, combination): Q_k = sum_v v B_v by running sums
+// from v = 6 down over the folded buckets, stored over the combination's
+// first bucket (only this pair reads those buckets)
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_combine(DevBatch B, uint32_t n_sg) {
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (w >= n_sg * SGB_K) return;
@@ -123,9 +139,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_combine(DevBatch B, uint32_t 
   bool exc = false;
 #pragma unroll 1
   for (int v = (int)SGB_V; v >= 1; --v) {
-    const G2J* pb = part + (size_t)(v - 1) * SGB_SPLIT;
-#pragma unroll 1
-    for (uint32_t sl = 0; sl < SGB_SPLIT; ++sl) run = jac_add_x(run, px_load(pb[sl]), exc);
+    run = jac_add_x(run, px_load(part[(size_t)(v - 1) * SGB_SPLIT]), exc);
     q = jac_add_x(q, run, exc);
   }
   if (pair_all(!exc)) px_store(part[0], q);
@@ -161,6 +175,7 @@ void launch_subgroup_batch(const DevBatch& B, hipStream_t st) {
   if (!B.sgb || !n_sg) return;
   TBG_KLAUNCH(k_sgb_sort, dim3(n_sg), dim3(kSgbSortBlock), st, B);
   TBG_KLAUNCH(k_sgb_bucket, grid_for(2 * n_sg * SGB_BUCKETS * SGB_SPLIT), dim3(kBlock), st, B, n_sg);
+  if (SGB_SPLIT > 1) TBG_KLAUNCH(k_sgb_fold, grid_for(2 * n_sg * SGB_BUCKETS), dim3(kBlock), st, B, n_sg);
   TBG_KLAUNCH(k_sgb_combine, grid_for(2 * n_sg * SGB_K), dim3(kBlock), st, B, n_sg);
   TBG_KLAUNCH(k_sgb_test, grid_for(2 * n_sg * SGB_K), dim3(kBlock), st, B, n_sg);
 }

@@ -146,9 +146,10 @@ def main():
     madd, _ = measure(lib.hc_k_msm_entry, 0)  # k = 0: psi^0, one mixed addition
     sgb_m, sgb_k = 512, 18
     sgb_bucket = sgb_k * 12 / 13 * madd
-    sgb_combine = sgb_k * 30 * g2_add / sgb_m
+    sgb_fold = sgb_k * 6 * 3 * g2_add / sgb_m  # each bucket's 4 slices into one
+    sgb_combine = sgb_k * 12 * g2_add / sgb_m  # the running sums over the 6 folded buckets
     sgb_test = sgb_k * (k_subgroup + 5 * (g2_add - madd)) / sgb_m
-    sgb_per_partial = sgb_bucket + sgb_combine + sgb_test
+    sgb_per_partial = sgb_bucket + sgb_fold + sgb_combine + sgb_test
     decode_sgb = k_decode + sgb_per_partial
     l0_per_group = nch * chunk2 + nch * qmul
     l0_per_launch = bucket_scales + (32768 + 2048 + 128 + 8) * g2_add + lines_h + s_quad + final1
@@ -201,6 +202,7 @@ def main():
             "k_decode_sigs": {"per": "partial", "mads": round(k_decode)},
             "k_subgroup_sigs": {"per": "partial", "mads": round(k_subgroup)},
             "k_sgb_bucket": {"per": "partial", "mads": round(sgb_bucket)},
+            "k_sgb_fold": {"per": "partial", "mads": round(sgb_fold)},
             "k_sgb_combine": {"per": "partial", "mads": round(sgb_combine)},
             "k_sgb_test": {"per": "partial", "mads": round(sgb_test)},
             "k_hash_map": {"per": "message", "mads": round(k_hash_map)},
