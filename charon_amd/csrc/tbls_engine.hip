@@ -134,7 +134,7 @@ struct tbg_ctx {
   uint32_t fb_window = TBG_FB_WINDOW;  // fallback line buffer positions per pass (tbg_config.fb_window)
   uint32_t sgb_mode = TBG_SGB_AUTO;    // batched subgroup test (tbg_config.subgroup_batch)
   uint32_t express_max = TBG_EXPRESS_PARTIALS;  // batches up to this many partials prefer the express slot
-  uint32_t hex_slots = 2048;  // Miller-hexad waves the device runs at once (CUs x 4 SIMDs x TBG_HEX_WAVES)
+  uint32_t n_simd = 1024;  // SIMDs of the device (CUs x 4): the level-0 shape rule's unit (l0_shape)
   // host-side work of the submit / collect calls (tbg_host_stats): [submits,
   // partials submitted, pack ns, enqueue ns, collects, partials collected,
   // gather ns, wait ns]
@@ -254,7 +254,7 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   c->slots.resize(nslots + (express ? 1 : 0));
   int n_cu = 0;
   if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n_cu > 0)
-    c->hex_slots = (uint32_t)n_cu * 4u * 2u;  // two hexad waves per SIMD (bls_hex.h TBG_HEX_WAVES)
+    c->n_simd = (uint32_t)n_cu * 4u;
   // One stream per slot by default: the HIP runtime maps streams onto a
   // few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), so concurrency
   // comes from several batches in flight, one queue each.  Two streams
@@ -535,39 +535,50 @@ static Slot* find_ticket(tbg_ctx* c, tbg_ticket t, bool want_pending, Part** par
 int tbg_submit(tbg_ctx* c, const tbg_batch* b, tbg_ticket* ticket) { return tbg_submit_group(c, &b, 1, ticket); }
 
 // Level-0 launch shape.  The level-0 Miller kernel's
-// waves are long (one hexad = the whole 68-step loop over C duties, ~6 ms
-// at C = 4) and all alike, so its time is set by rounds of the device's
-// two-wave slots: config 4's 125k-duty shard at (G, C) = (16, 4) is 3,126
-// waves, 1.53 rounds of 2,048 slots.  A hexad of C duties costs 62
-// squarings + 68 C line products, w(C) = 0.95 M + 1.39 M C u32 mul-adds
-// (profiles/work_model.json, l0_chunk_*), so fewer, longer hexads win
-// where they save a round: (16, 8) halves the squarings, (14, 7) runs 125k
-// duties in 0.87 of a round.  The kernel's time is modelled as w(C) x
-// (whole rounds + min(1, 0.25 + 1.25 x the last round's fill)): a partly
-// filled last round runs its waves with the SIMDs to themselves (fitted to
-// the six A/B points of profiles/r05/chunk8_ab, shape_ab, sqrt_x2_ab within
-// 4 %: 100k duties keep (16, 4), 125k take (14, 7), 160k (16, 8)).  A
-// configured group size G keeps G (C = 4 or 8 only).
-static double l0_shape_cost(uint32_t nd, uint32_t slots, uint32_t g, uint32_t ch) {
+// waves are long -- one hexad = the whole 68-step loop over C duties -- and
+// issue-bound at ONE wave per SIMD: a lone wave runs its loop in 3.6 ms at
+// C = 4, two sharing a SIMD take 6.8 ms each (profiles/r05/waves), so the
+// kernel's time is ~ceil(waves / SIMDs) hexad lengths, and a launch whose
+// waves spill just past a multiple of the SIMD count pays a whole hexad
+// length for the remainder: config 4's 125k-duty shard at (G, C) = (16, 4)
+// is 3,126 waves on 1,024 SIMDs.  A hexad of C duties costs 62 squarings +
+// 68 C line products, w(C) = 0.95 M + 1.39 M C u32 mul-adds
+// (profiles/work_model.json, l0_chunk_*), so fewer, longer hexads win where
+// they save a unit: (16, 8) halves the squarings, (14, 7) runs 125k duties
+// in 2 units instead of 4.  The rule picks the cheapest of (16, 4), (16, 8),
+// (14, 7) by ceil(waves / SIMDs) x w(C) -- 100k duties keep (16, 4), 125k
+// take (14, 7), 160k (16, 8), as the A/B runs of profiles/r05/chunk8_ab,
+// shape_ab and sqrt_x2_ab measured best.  A configured group size G keeps G
+// (C = 4 or 8 only).  tbg_replay_plan applies it to the duties of the
+// launches it runs together (their Miller kernels share the SIMDs).
+static double l0_shape_cost(uint64_t nd, uint32_t n_simd, uint32_t g, uint32_t ch) {
   const uint64_t hexads = (uint64_t)((nd + g - 1) / g) * ((g + ch - 1) / ch);
-  const double r = (double)((hexads + 9) / 10) / (double)slots;
-  const double whole = (double)(uint64_t)r, part = r - whole;
-  return (0.948 + 1.395 * ch) * (whole + (part > 0 ? std::min(1.0, 0.25 + 1.25 * part) : 0.0));
+  const uint64_t waves = (hexads + 9) / 10;
+  return (0.948 + 1.395 * ch) * (double)((waves + n_simd - 1) / n_simd);
 }
-static void l0_shape(uint32_t nd, uint32_t slots, bool g_free, uint32_t& G, uint32_t& C) {
+static void l0_shape(uint64_t nd, uint32_t n_simd, bool g_free, uint32_t& G, uint32_t& C) {
   const uint32_t cand[3][2] = {{g_free ? 16u : G, 4}, {g_free ? 16u : G, 8}, {14, 7}};
   C = 4;
   if (!TBG_L0_SHAPE || G < 8) return;
   const uint32_t G0 = G;
-  double best = l0_shape_cost(nd, slots, G0, 4);
+  double best = l0_shape_cost(nd, n_simd, G0, 4);
   for (uint32_t k = 1; k < (g_free ? 3u : 2u); ++k) {
-    const double cost = l0_shape_cost(nd, slots, cand[k][0], cand[k][1]);
+    const double cost = l0_shape_cost(nd, n_simd, cand[k][0], cand[k][1]);
     if (cost < best) {
       best = cost;
       G = cand[k][0];
       C = cand[k][1];
     }
   }
+}
+// A launch of nd duties (a prefix of its slot's device batch) at (G, C) fits
+// the slot's arena, whose group / chunk sections were sized at submit for
+// the slot's nd0 duties at (G0, C0) (tbg_submit_group).
+static bool l0_shape_fits(uint32_t nd0, uint32_t G0, uint32_t C0, uint32_t nd, uint32_t G, uint32_t C) {
+  const uint64_t ng0 = (nd0 + G0 - 1) / G0, nch0 = (G0 + C0 - 1) / C0;
+  const uint64_t ng = (nd + G - 1) / G, nch = (G + C - 1) / C;
+  return ng <= ng0 && ng * (nch + 1) <= ng0 * (nch0 + 1) && ng * nch * C <= ng0 * nch0 * C0 && ng * G <= ng0 * G0 &&
+         std::max(ng * nch, (uint64_t)nd) <= std::max(ng0 * nch0, (uint64_t)nd0) && (G <= 64) == (G0 <= 64);
 }
 
 int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches, tbg_ticket* tickets) {
@@ -641,7 +652,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   const bool l0 = G != 0 && np < (1u << 28) &&
                   (c->rlc_batch == TBG_RLC_L0_ON || (c->rlc_batch == TBG_RLC_L0_AUTO && c->invalid_ema < TBG_RLC_AUTO_L0));
   uint32_t C = c->rlc_chunk;
-  if (l0 && c->chunk_auto) l0_shape(nd, c->hex_slots, c->rlc_auto && G == 16, G, C);
+  if (l0 && c->chunk_auto) l0_shape(nd, c->n_simd, c->rlc_auto && G == 16, G, C);
   if (C > G) C = G ? G : 1;
   const uint32_t ng = G ? (nd + G - 1) / G : 0;
   const uint32_t nch = G ? (G + C - 1) / C : 0;
@@ -1061,6 +1072,25 @@ int tbg_replay_plan(tbg_ctx* c, const tbg_ticket* tickets, const uint32_t* n_par
   for (uint32_t k0 = 0; k0 < n_launches && rc == TBG_OK;) {
     uint32_t k1 = k0 + 1;
     while (k1 < n_launches && std::find(sl.begin() + k0, sl.begin() + k1, sl[k1]) == sl.begin() + k1) ++k1;
+#if TBG_REPLAY_SHAPE
+    // The level-0 launches run together share the SIMDs: their shape follows
+    // their duties together (l0_shape), where each launch's arena fits it.
+    if (c->chunk_auto && c->rlc_auto) {
+      uint64_t nd = 0;
+      bool all_l0 = true;
+      for (uint32_t k = k0; k < k1; ++k) {
+        nd += bs[k].n_duties;
+        all_l0 = all_l0 && bs[k].rlc_batch && bs[k].rlc_group >= 8;
+      }
+      uint32_t G = 16, C = 4;
+      if (all_l0) l0_shape(nd, c->n_simd, true, G, C);
+      for (uint32_t k = k0; k < k1 && all_l0; ++k)
+        if (l0_shape_fits(sl[k]->n_duties, sl[k]->B.rlc_group, sl[k]->B.rlc_chunk, bs[k].n_duties, G, C)) {
+          bs[k].rlc_group = G;
+          bs[k].rlc_chunk = C;
+        }
+    }
+#endif
     for (int stage = 0; stage < 3 && rc == TBG_OK; ++stage)
       for (uint32_t k = k0; k < k1 && rc == TBG_OK; ++k)
         rc = launch_chain(c, *sl[k], bs[k], ev.data() + (size_t)kChainEvents * k, stage);

@@ -17,6 +17,11 @@ constexpr int kBlock = 64;
 // need more than one round of the device's wave slots picks (G, C) among
 // (16, 4), (16, 8), (14, 7) by rounds x hexad length (tbls_engine.hip,
 // l0_shape); 0: always (16, 4).
+// tbg_replay_plan: the launches a plan runs together take the level-0 shape
+// of their duties together (1), or keep their submitted shapes (0)
+#ifndef TBG_REPLAY_SHAPE
+#define TBG_REPLAY_SHAPE 1
+#endif
 #ifndef TBG_L0_SHAPE
 #define TBG_L0_SHAPE 1
 #endif

@@ -17,15 +17,12 @@ DVS = 125000
 
 def expected_shape(nd, n_cu, g_free=True, G=16):
     """Mirror of l0_shape: the hexad cost 0.948 + 1.395 C (M u32 mul-adds,
-    profiles/work_model.json) x (whole rounds of the CUs x 4 SIMDs x 2 wave
-    slots + min(1, 0.25 + 1.25 x the last round's fill))."""
-    slots = n_cu * 8
+    profiles/work_model.json) x ceil(waves / SIMDs), SIMDs = CUs x 4."""
+    n_simd = n_cu * 4
 
     def cost(g, c):
-        r = -(-(-(-nd // g) * -(-g // c)) // 10) / slots
-        whole = int(r)
-        part = r - whole
-        return (0.948 + 1.395 * c) * (whole + (min(1.0, 0.25 + 1.25 * part) if part > 0 else 0.0))
+        waves = -(-(-(-nd // g) * -(-g // c)) // 10)
+        return (0.948 + 1.395 * c) * -(-waves // n_simd)
 
     if G < 8:
         return G, 4
@@ -43,6 +40,9 @@ def test_shape_mirror():
     assert expected_shape(10000, 256) == (16, 4)
     assert expected_shape(100000, 256) == (16, 4)  # config 3's launch (1.22 rounds at C = 4)
     assert expected_shape(125000, 256, g_free=False, G=16) == (16, 8)
+    # the 20-step bench plan: 7 + 7 + 6 batches replayed together
+    assert expected_shape(200000, 256) == (14, 7)
+    assert expected_shape(480000, 256) == (16, 8)
 
 
 @pytest.fixture(scope="module")
