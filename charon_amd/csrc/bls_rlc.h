@@ -127,6 +127,62 @@ TBG_HD Jac<F> rlc_mul_table(const Aff<F>& ap, const Aff<F>& am, const Fp& c, con
   return acc;
 }
 
+// Per-key window table (k_pubkey_tables): the eight points e0 q0 + e1 q1,
+// e0 in {1, 3}, e1 in {-3, -1, 1, 3} (q0 = pk, q1 = [x]pk), at index
+// 4 (e0 == 3) + (e1 + 3) / 2.  Two bits of each of two digits (bit set ->
+// +1, clear -> -1, as above) select one entry +-e0 q0 +- e1 q1 (the sign of
+// e0 moved to y), so [r] pk takes 14 doublings + 16 additions instead of
+// the pair table's 15 + 32 -- for a table resident per key (896 bytes).
+constexpr uint32_t PK_TAB_W2 = 8;
+template <class F>
+TBG_HD Jac<F> rlc_key_table_w2_entry(const Aff<F>& q0, const Aff<F>& q1, int k) {
+  const int e0 = k >= 4 ? 3 : 1, e1 = 2 * (k & 3) - 3;
+  const Jac<F> a = jac_from_aff(q0), b = jac_from_aff(q1);
+  Jac<F> p0 = e0 == 3 ? jac_add(jac_dbl(a), a) : a;
+  Jac<F> p1 = (e1 == 3 || e1 == -3) ? jac_add(jac_dbl(b), b) : b;
+  if (e1 < 0) p1 = jac_neg(p1);
+  return jac_add(p0, p1);
+}
+// the window of bits 2i + 1, 2i of a digit: 2 (+-1) + (+-1)
+TBG_HD int rlc_win2(uint32_t u, int i) {
+  return 2 * (2 * (int)((u >> (2 * i + 1)) & 1u) - 1) + (2 * (int)((u >> (2 * i)) & 1u) - 1);
+}
+template <class F>
+TBG_HD Aff<F> rlc_entry_w2(const Aff<F>* tab, int v0, int v1, bool endo, const Fp& c) {
+  const bool neg = v0 < 0;
+  if (neg) {
+    v0 = -v0;
+    v1 = -v1;
+  }
+  Aff<F> e = tab[(v0 == 3 ? 4 : 0) + (v1 + 3) / 2];
+  if (neg != endo) e.y = f_reduce(f_neg(e.y));  // endo maps (x, y) -> (c x, -y)
+  if (endo) e.x = rlc_mul_c(e.x, c);
+  return e;
+}
+template <class F>
+TBG_HD Jac<F> rlc_mul_key_w2(const Aff<F>* tab, const Fp& c, const uint32_t (&u)[4]) {
+  Jac<F> acc = jac_from_aff(rlc_entry_w2(tab, rlc_win2(u[0], 7), rlc_win2(u[1], 7), false, c));
+  acc = jac_add_aff_in(acc, rlc_entry_w2(tab, rlc_win2(u[2], 7), rlc_win2(u[3], 7), true, c));
+#pragma unroll 1
+  for (int i = 6; i >= 0; --i) {
+    acc = jac_dbl_in(jac_dbl_in(acc));
+    acc = jac_add_aff_in(acc, rlc_entry_w2(tab, rlc_win2(u[0], i), rlc_win2(u[1], i), false, c));
+    acc = jac_add_aff_in(acc, rlc_entry_w2(tab, rlc_win2(u[2], i), rlc_win2(u[3], i), true, c));
+  }
+  return acc;
+}
+
+// [r] pk from the key's resident table (PK_TAB entries, tbls_launch.h)
+#if defined(TBG_PK_W2)
+TBG_HD G1J rlc_mul_key(const G1A* tab, const uint32_t (&u)[4]) {
+#if TBG_PK_W2
+  return rlc_mul_key_w2(tab, fp_from_const(G1_BETA), u);
+#else
+  return rlc_mul_table(tab[0], tab[1], fp_from_const(G1_BETA), u);
+#endif
+}
+#endif
+
 // [r] s for s in G2 (affine): pairs (s, psi(s)) and psi^2 of the same table.
 TBG_HD G2J rlc_mul_g2(const G2A& s, const uint32_t (&u)[4]) {
   const G2A ps = g2_psi_aff(s);

@@ -29,8 +29,10 @@
 
 namespace tbg {
 
-// Pair table of every usable key (k_rlc_g1_l0): A+ = pk + [x]pk, A- = pk - [x]pk
-// (the slope's inversion batched over the workgroup, bls_batchinv.h).
+// Table of every usable key (k_rlc_g1_l0, k_rlc_partial2): the window table
+// of bls_rlc.h (TBG_PK_W2: e0 pk + e1 [x]pk, e0 in {1, 3}, e1 in {+-1, +-3})
+// or the pair table A+ = pk + [x]pk, A- = pk - [x]pk, each entry's affine
+// conversion batched over the workgroup (bls_batchinv.h).
 __global__ void __launch_bounds__(BINV_BLOCK) k_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status,
                                                               uint32_t n, G1A* tab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -41,6 +43,17 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_pubkey_tables(const G1A* pk, con
     p0 = pk[i];
     x0 = xpk[i];
   }
+#if TBG_PK_W2
+  // e0 pk + e1 [x]pk is never the identity for a prime-order key (it would
+  // need x = -e0 / e1 mod r); every thread runs every batched conversion
+#pragma unroll 1
+  for (int k = 0; k < (int)PK_TAB; ++k) {
+    const G1J e = ok ? rlc_key_table_w2_entry(p0, x0, k) : jac_inf<Fp>();
+    G1A a{fp_zero(), fp_zero()};
+    const bool got = block_jac_to_aff<BINV_WAVES>(e, ok, a);
+    if (in) tab[(size_t)PK_TAB * i + k] = got ? a : G1A{fp_zero(), fp_zero()};
+  }
+#else
   // x0.x != p0.x for a prime-order key ([x]pk = +-pk would need x = +-1 mod r)
   const Fp t = block_batch_inv<BINV_WAVES>(fp_reduce(fp_sub(x0.x, p0.x)), ok);  // every thread of the workgroup
   if (!in) return;
@@ -48,6 +61,7 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_pubkey_tables(const G1A* pk, con
   if (ok) rlc_pair_from_inv(p0, x0, t, ap, am);
   tab[2ull * i] = ap;
   tab[2ull * i + 1] = am;
+#endif
 }
 
 // Level-0 G1 side, one lane per partial: unusable keys are marked, every
@@ -66,7 +80,7 @@ __global__ void TBG_LAUNCH k_rlc_g1_l0(DevBatch B, const G1A* tab, const int32_t
   uint32_t u[4];
   rlc_digits(r, u);
   B.msm_r[i] = r;
-  B.part_p[i] = rlc_mul_table(tab[2ull * pid], tab[2ull * pid + 1], fp_from_const(G1_BETA), u);
+  B.part_p[i] = rlc_mul_key(tab + (size_t)PK_TAB * pid, u);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     bool neg;

@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(BINV_BLOCK, TBG_PAIR_WAVES) k_rlc_partial2(Dev
     rlc_digits(rlc_scalar(B.rlc_seed, i), a);
     const G2A s = B.sig_aff[i];
     dx2 = fp2_reduce(fp2_sub(fp2_mul(fp2_conj(s.x), fp2_from_const(PSI_X)), s.x));  // psi(s).x - s.x
-    if (!B.rlc_batch) B.part_p[i] = rlc_mul_table(pk_tab[2ull * pid], pk_tab[2ull * pid + 1], fp_from_const(G1_BETA), a);
+    if (!B.rlc_batch) B.part_p[i] = rlc_mul_key(pk_tab + (size_t)PK_TAB * pid, a);
   }
   const Fp2 inv2 = block_batch_inv2<BINV_WAVES>(dx2, work);  // every thread of the workgroup
   for (uint32_t j = 0; j < 2; ++j) {

@@ -111,7 +111,7 @@ struct tbg_ctx {
   std::mutex mu;
   G1A* d_pk = nullptr;
   G1A* d_xpk = nullptr;  // [x] pk per entry (k_decode_pubkeys)
-  G1A* d_pktab = nullptr;  // [2 per entry] pk + [x]pk, pk - [x]pk (level 0's G1 products, k_msm.hip)
+  G1A* d_pktab = nullptr;  // [PK_TAB per key] the RLC products' key tables (k_msm.hip k_pubkey_tables)
   int32_t* d_pk_status = nullptr;
   uint32_t n_pk = 0, cap_pk = 0;
   hipEvent_t retire_ev = nullptr;  // orders frees of outgrown pubkey tables after the slots' queued work
@@ -343,7 +343,7 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
       hipFreeAsync(npk, us);
       return TBG_E_OOM;
     }
-    if (hipMallocAsync((void**)&ntab, 2 * sizeof(G1A) * (size_t)ncap, us) != hipSuccess) {
+    if (hipMallocAsync((void**)&ntab, PK_TAB * sizeof(G1A) * (size_t)ncap, us) != hipSuccess) {
       hipFreeAsync(npk, us);
       hipFreeAsync(nxpk, us);
       return TBG_E_OOM;
@@ -357,7 +357,7 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
     if (c->n_pk) {
       HIP_TRY(hipMemcpyAsync(npk, c->d_pk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
       HIP_TRY(hipMemcpyAsync(nxpk, c->d_xpk, sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
-      HIP_TRY(hipMemcpyAsync(ntab, c->d_pktab, 2 * sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
+      HIP_TRY(hipMemcpyAsync(ntab, c->d_pktab, PK_TAB * sizeof(G1A) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
       HIP_TRY(hipMemcpyAsync(nst, c->d_pk_status, sizeof(int32_t) * (size_t)c->n_pk, hipMemcpyDeviceToDevice, us));
     }
     old_tabs[0] = c->d_pk;
@@ -379,7 +379,7 @@ int tbg_load_pubkeys(tbg_ctx* c, const uint8_t* pk48, uint32_t count, uint32_t* 
   if (rc == TBG_OK) {
     launch_decode_pubkeys(d_bytes, count, c->d_pk + c->n_pk, c->d_xpk + c->n_pk, c->d_pk_status + c->n_pk, c->stream);
     launch_pubkey_tables(c->d_pk + c->n_pk, c->d_xpk + c->n_pk, c->d_pk_status + c->n_pk, count,
-                         c->d_pktab + 2ull * c->n_pk, c->stream);
+                         c->d_pktab + (size_t)PK_TAB * c->n_pk, c->stream);
     if (hipGetLastError() != hipSuccess) rc = TBG_E_DEVICE;
   }
   if (rc == TBG_OK && status &&

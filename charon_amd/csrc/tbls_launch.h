@@ -17,6 +17,13 @@ constexpr int kBlock = 64;
 // need more than one round of the device's wave slots picks (G, C) among
 // (16, 4), (16, 8), (14, 7) by rounds x hexad length (tbls_engine.hip,
 // l0_shape); 0: always (16, 4).
+// Per-key G1 tables for the RLC products [r_i] pk_i: 1 = the 8-entry window
+// table (bls_rlc.h rlc_mul_key_w2: 14 doublings + 16 additions), 0 = the
+// 2-entry pair table pk +- [x]pk (15 + 32)
+#ifndef TBG_PK_W2
+#define TBG_PK_W2 1
+#endif
+constexpr uint32_t PK_TAB = TBG_PK_W2 ? 8u : 2u;  // G1A entries per key in the resident table
 // tbg_replay_plan: the launches a plan runs together take the level-0 shape
 // of their duties together (1), or keep their submitted shapes (0)
 #ifndef TBG_REPLAY_SHAPE

@@ -331,8 +331,9 @@ int tbg_last_timings(const tbg_ctx* ctx, float* ms8);
  * engine is initialised from the app wiring (app/app.go:321-488).
  *
  * Public keys are replicated: tbg_multi_load_pubkeys decodes the table on
- * every device (1 M DVs x 4 shares x 452 B ~ 1.8 GB, 0.6 % of a GPU's 288
- * GB: pk, [x]pk and level 0's pair table, 4 x 112 B of affine G1, + status), so any shard can reference any id and the ids are the same as for a
+ * every device (1 M DVs x 4 shares x 1,124 B ~ 4.5 GB, 1.6 % of a GPU's 288
+ * GB: pk, [x]pk and the RLC products' 8-entry window table, 10 x 112 B of
+ * affine G1, + status), so any shard can reference any id and the ids are the same as for a
  * single context.  Replication is the chosen design: the cut follows the
  * partial counts of whatever batches arrive (a burst of one committee's
  * duties still spreads over every GPU), where key-owned shards would route

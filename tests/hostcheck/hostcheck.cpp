@@ -704,6 +704,21 @@ int hc_pair_decode_sig(const uint8_t* sig96) {
 }
 }
 
+// [r] pk from the per-key window table (bls_rlc.h rlc_mul_key_w2, the table
+// built entry by entry as k_pubkey_tables does) against the plain
+// double-and-add [r mod order] pk: 1 on a match.
+extern "C" int hc_rlc_check_w2(const uint8_t* pk48, uint64_t r64, const uint32_t* r_words) {
+  G1A pk;
+  if (g1_decompress(pk48, pk) != DEC_OK) return -1;
+  uint32_t a[4];
+  rlc_digits(r64, a);
+  const G1A xpk = hc_xpk(pk);
+  G1A tab[PK_TAB_W2];
+  for (int k = 0; k < (int)PK_TAB_W2; ++k)
+    if (!jac_to_aff(rlc_key_table_w2_entry(pk, xpk, k), tab[k])) return -2;
+  return jac_eq(rlc_mul_key_w2(tab, fp_from_const(G1_BETA), a), jac_mul_words(jac_from_aff(pk), r_words, 255)) ? 1 : 0;
+}
+
 // Inversion-free RLC products (bls_rlc.h *_j, the split kernels k_rlc_g1 /
 // k_rlc_g2_pair): G1, single-lane G2 and the pair-emulated G2, each against
 // the plain 255-bit double-and-add [r mod order] P.  Bits 1 | 2 | 4.

@@ -308,6 +308,10 @@ def test_rlc_digit_scalars_match_plain_scalar_multiplication():
         L.hc_rlc_check_j.restype = ctypes.c_int
         L.hc_rlc_check_j.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
         assert L.hc_rlc_check_j(sig, pk, r64, words) == 7
+        # the per-key window table of level 0 / the group levels (k_pubkey_tables)
+        L.hc_rlc_check_w2.restype = ctypes.c_int
+        L.hc_rlc_check_w2.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+        assert L.hc_rlc_check_w2(pk, r64, words) == 1
 
 
 def test_base_x_msm_matches_plain_scalar_multiplication():
