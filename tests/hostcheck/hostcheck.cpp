@@ -789,16 +789,20 @@ int hc_msm_check(const uint8_t* sigs96, const uint64_t* r, uint32_t n) {
 // key's pair table plus its 4 bucket additions; the G1-only duty sum; one
 // bucket's [2j + 1]; one tree addition.
 extern "C" {
+// the key's window table (k_pubkey_tables), built at key load
+static void hc_key_table_w2(G1A (&tab)[PK_TAB_W2]) {
+  for (int k = 0; k < (int)PK_TAB_W2; ++k) jac_to_aff(rlc_key_table_w2_entry(g_pk, g_xpk, k), tab[k]);
+}
 void hc_stage_l0_partial(uint64_t r64) {
-  G1A ap, am;
-  rlc_pair_from_inv(g_pk, g_xpk, fp_inv(fp_reduce(fp_sub(g_xpk.x, g_pk.x))), ap, am);  // at key load
+  G1A tab[PK_TAB_W2];
+  hc_key_table_w2(tab);  // at key load
   G2J acc = jac_dbl(jac_from_aff(g_sig));
 #if defined(TBG_COUNT_OPS)
   tbg_mad_count = 0;
 #endif
   uint32_t u[4];
   rlc_digits(r64, u);
-  G1J P = rlc_mul_table(ap, am, fp_from_const(G1_BETA), u);
+  G1J P = rlc_mul_key_w2(tab, fp_from_const(G1_BETA), u);
   (void)P;
   for (uint32_t k = 0; k < 4; ++k) {
     bool neg;
@@ -902,14 +906,14 @@ void hc_k_g2_affine(void) {
 }
 // k_rlc_g1_l0: [r] pk from the key's pair table (the bucket additions are k_msm_bucket_part's)
 void hc_k_rlc_g1_l0(uint64_t r64) {
-  G1A ap, am;
-  rlc_pair_from_inv(g_pk, g_xpk, fp_inv(fp_reduce(fp_sub(g_xpk.x, g_pk.x))), ap, am);  // at key load
+  G1A tab[PK_TAB_W2];
+  hc_key_table_w2(tab);  // at key load
 #if defined(TBG_COUNT_OPS)
   tbg_mad_count = 0;
 #endif
   uint32_t u[4];
   rlc_digits(r64, u);
-  (void)rlc_mul_table(ap, am, fp_from_const(G1_BETA), u);
+  (void)rlc_mul_key_w2(tab, fp_from_const(G1_BETA), u);
 }
 // k_msm_bucket_part: one bucket entry (psi^k of a signature, one mixed addition)
 void hc_k_msm_entry(uint32_t k) {
