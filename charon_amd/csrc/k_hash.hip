@@ -3,7 +3,7 @@
 // allows (bls_pair.h):
 //   k_hash_map     one lane per message: expand_message_xmd, hash_to_field,
 //                  the two SSWU maps and 3-isogenies (Fp exponentiations),
-//                  Q = Q0 + Q1 (Jacobian) into h_jac;
+//                  Q0 and Q1 (Jacobian) into h_jac (k_hash_clear_x1 adds them);
 //   k_hash_clear   one lane per message: Budroni-Pintore cofactor clearing
 //                  (one wave per SIMD: three live G2 points);
 //   k_hash_affine  one lane per message: to affine (inversion batched over
@@ -35,7 +35,11 @@ __global__ void __launch_bounds__(BINV_BLOCK, TBG_DECODE_WAVES) k_hash_map(DevBa
   if (!in) return;
   G2J q0, q1;
   sswu_pair_finish(u0, u1, w, ok, di, q0, q1);
-  B.h_jac[m] = jac_add(q0, q1);
+  // Q0 + Q1 is the first step of k_hash_clear_x1 (a lane pair per message):
+  // here the out-of-line G2 addition saved and restored ~360 callee-saved
+  // VGPR words through scratch per message
+  B.h_jac[m] = q0;
+  B.h_jac[B.n_msgs + m] = q1;
 }
 
 __global__ void __launch_bounds__(BINV_BLOCK, TBG_DECODE_WAVES) k_hash_affine(DevBatch B) {

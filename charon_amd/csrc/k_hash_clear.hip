@@ -5,7 +5,7 @@
 // in three lane-PAIR kernels (bls_pair.h: the Fp2 coordinates split over two
 // lanes) so each holds at most two G2 points across its [x] loop and runs two
 // waves per SIMD:
-//   k_hash_clear_x1   t1 = [x]P, u = t1 + psi(P)      (temporaries in h_jac)
+//   k_hash_clear_x1   P = Q0 + Q1, t1 = [x]P, u = t1 + psi(P)  (temporaries in h_jac)
 //   k_hash_clear_x2   v = [x]u
 //   k_hash_clear_fin  h = psi^2(2P) - psi(P) + v - t1 - P
 // The single-lane form kept three live points across the second [x] loop and
@@ -53,7 +53,9 @@ __device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x1(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (m >= B.n_msgs) return;
-  const Jac<Fp2x> p = px_load(B.h_jac[m]);
+  // P = Q0 + Q1, the two SSWU maps' points (k_hash_map)
+  const Jac<Fp2x> p = jac_add_in<Fp2x, true>(px_load(B.h_jac[m]), px_load(B.h_jac[B.n_msgs + m]));
+  px_store(B.h_jac[m], p);
   const Jac<Fp2x> t1 = px_mul_x(p);
   px_store(B.h_jac[B.n_msgs + m], t1);
   px_store(B.h_jac[2 * B.n_msgs + m], jac_add_in<Fp2x, true>(t1, px_psi(p)));

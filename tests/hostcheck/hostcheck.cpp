@@ -876,18 +876,18 @@ void hc_k_hash_map(const uint8_t* msg, uint32_t len) {
   hash_to_field_fp2(msg, len, u0, u1);
   G2J q0, q1;
   map_to_curve_g2_pair(u0, u1, q0, q1);
-  (void)jac_add(q0, q1);
+  (void)q0;
+  (void)q1;
 }
-// k_hash_clear_x1 / _x2 / _fin on the message's mapped point
-static G2J g_hq, g_ht1, g_hu;
+// k_hash_clear_x1 / _x2 / _fin on the message's two mapped points
+static G2J g_hq, g_hq0, g_hq1, g_ht1, g_hu;
 void hc_k_hash_clear_setup(const uint8_t* msg, uint32_t len) {
   Fp2 u0, u1;
   hash_to_field_fp2(msg, len, u0, u1);
-  G2J q0, q1;
-  map_to_curve_g2_pair(u0, u1, q0, q1);
-  g_hq = jac_add(q0, q1);
+  map_to_curve_g2_pair(u0, u1, g_hq0, g_hq1);
 }
 void hc_k_hash_clear_x1(void) {
+  g_hq = jac_add_in<Fp2, true>(g_hq0, g_hq1);  // Q0 + Q1 (moved here from k_hash_map)
   g_ht1 = jac_neg(jac_mul_xabs_in2(g_hq));
   g_hu = jac_add_in<Fp2, true>(g_ht1, g2_psi(g_hq));
 }

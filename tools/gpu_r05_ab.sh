@@ -32,7 +32,7 @@ for rep in 1 2; do
     libenv $(arm_lib $A)
     f=$O/${n}_s20_$rep.json
     timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu --api-batches 0 --latency 0 $(arm_args $A) > $f 2> $f.err || { tail -20 $f.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$f'));k=d['isolated_kernel_ms'];print('$n s20 $rep', d['value'], d['roofline']['frac'], {x: k[x] for x in k if 'miller' in x or 'decode' in x or 'sgb' in x})"
+    python3 -c "import json;d=json.load(open('$f'));k=d['isolated_kernel_ms'];print('$n s20 $rep', d['value'], d['roofline']['frac'], {x: k[x] for x in k if 'miller' in x or 'hash' in x})"
   done
 done
 if [ "${C3:-1}" = 1 ]; then
@@ -41,7 +41,7 @@ if [ "${C3:-1}" = 1 ]; then
     libenv $(arm_lib $A)
     f=$O/${n}_c3.json
     timeout -k 10 300 python3 -u bench.py --workload config3 --steps 6 --warmup 2 --no-cpu --api-batches 0 --latency 0 $(arm_args $A) > $f 2> $f.err || { tail -20 $f.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$f'));k=d['isolated_kernel_ms'];print('$n c3', d['value'], {x: k[x] for x in k if 'miller' in x or 'decode' in x or 'sgb' in x})"
+    python3 -c "import json;d=json.load(open('$f'));k=d['isolated_kernel_ms'];print('$n c3', d['value'], {x: k[x] for x in k if 'miller' in x or 'hash' in x})"
   done
 fi
 unset TBG_LIB
