@@ -68,16 +68,34 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x2(DevBatch B) {
   px_store(*u, px_mul_x(px_load(*u)));
 }
 
+// The combination with the complete additions (out-of-line calls): the rare
+// doubling case of the fast path below, out of line so its registers do not
+// count against the kernel's body.
+__device__ __noinline__ Jac<Fp2x> clear_fin_complete(const DevBatch& B, uint32_t m) {
+  const Jac<Fp2x> p = px_load(B.h_jac[m]);
+  Jac<Fp2x> t3 = px_psi(px_psi(jac_dbl(p)));                                    // psi^2(2P)
+  t3 = jac_add(t3, jac_neg(px_psi(p)));                                          // - psi(P)
+  t3 = jac_add(t3, px_load(B.h_jac[2 * B.n_msgs + m]));                          // + [x]([x]P + psi(P))
+  t3 = jac_add(t3, jac_neg(px_load(B.h_jac[B.n_msgs + m])));                     // - [x]P
+  return jac_add(t3, jac_neg(p));                                                // - P
+}
+
+// h = psi^2(2P) - [x]P + [x]([x]P + psi(P)) - psi(P) - P with the additions
+// that skip the doubling case (bls_pair.h jac_add_x) and psi(P) formed where
+// it is used: two live points instead of three (the complete form spilled
+// 654 VGPRs and wrote 4.5 KB of scratch per message)
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_fin(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (m >= B.n_msgs) return;
   const Jac<Fp2x> p = px_load(B.h_jac[m]);
-  const Jac<Fp2x> psi_p = px_psi(p);
-  Jac<Fp2x> t3 = px_psi(px_psi(jac_dbl_in(p)));                       // psi^2(2P)
-  t3 = jac_add_in<Fp2x, true>(t3, jac_neg(psi_p));                    // - psi(P)
-  t3 = jac_add_in<Fp2x, true>(t3, px_load(B.h_jac[2 * B.n_msgs + m]));  // + [x]([x]P + psi(P))
-  t3 = jac_add_in<Fp2x, true>(t3, jac_neg(px_load(B.h_jac[B.n_msgs + m])));  // - [x]P
-  px_store(B.h_jac[m], jac_add_in<Fp2x, true>(t3, jac_neg(p)));      // - P
+  bool exc = false;
+  Jac<Fp2x> t3 = px_psi(px_psi(jac_dbl_in(p)));                                 // psi^2(2P)
+  t3 = jac_add_x(t3, jac_neg(px_load(B.h_jac[B.n_msgs + m])), exc);             // - [x]P
+  t3 = jac_add_x(t3, px_load(B.h_jac[2 * B.n_msgs + m]), exc);                  // + [x]([x]P + psi(P))
+  t3 = jac_add_x(t3, jac_neg(px_psi(p)), exc);                                  // - psi(P)
+  t3 = jac_add_x(t3, jac_neg(p), exc);                                          // - P
+  if (!pair_all(!exc)) t3 = clear_fin_complete(B, m);  // (pair-uniform)
+  px_store(B.h_jac[m], t3);
 }
 
 void launch_hash_clear(const DevBatch& B, hipStream_t st) {
