@@ -34,13 +34,7 @@
 
 namespace tbg {
 
-// one workgroup per group of SGB_M partials; one wave (64) schedules as
-// soon as any SIMD slot frees under the other launches' long waves, where a
-// 256-thread group waits for four slots on one CU (A/B knob)
-#ifndef TBG_SGB_SORT_BLOCK
-#define TBG_SGB_SORT_BLOCK 64
-#endif
-constexpr uint32_t kSgbSortBlock = TBG_SGB_SORT_BLOCK;
+constexpr uint32_t kSgbSortBlock = 256;
 constexpr uint32_t SGB_ENT = SGB_M * SGB_K;  // entry capacity per group
 
 __global__ void __launch_bounds__(kSgbSortBlock) k_sgb_sort(DevBatch B) {
