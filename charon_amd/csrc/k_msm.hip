@@ -240,94 +240,6 @@ __global__ void __launch_bounds__(MSM_TREE_WG) k_msm_tree_final(DevBatch B) {
   px_store(*B.batch_pt, Aff<Fp2x>{f_mul(acc.X, zi2), f_mul(acc.Y, f_mul(zi2, zi))});
 }
 
-#if TBG_MSM_RC
-// The bucket scalings without a 16-bit scalar multiplication per bucket:
-// with j = 256 a + b (a < 128, b < 256) and 2j + 1 = 512 a + 2 b + 1,
-//   S = sum_j (2j + 1) B_j = sum_a T_a + [512] sum_a a T_a + [2] sum_b b U_b,
-// T_a = sum_b B_(256a+b) (row sums), U_b = sum_a B_(256a+b) (column sums):
-// 384 scalings by at most 8 bits instead of 32,768 by 16, at the same
-// dependent depth (~40 additions / doublings), ~10x less work.
-//   k_msm_bucket_sum  a lane pair per bucket: its slices' sum B_j (msm_bkt)
-//   k_msm_rowcol      a workgroup per row / column: T_a, U_b (msm_part[0, 384))
-//   k_msm_rcscale     a lane pair per row / column: a T_a, b U_b (msm_part[384, 768))
-//   k_msm_rcfinal     one workgroup: the three sums, S affine
-constexpr uint32_t MSM_RC_ROWS = 128, MSM_RC_COLS = 256, MSM_RC_PAIRS = 128;
-static_assert(MSM_RC_ROWS * MSM_RC_COLS == MSM_BUCKETS, "rows x columns");
-static_assert(2 * (MSM_RC_ROWS + MSM_RC_COLS) <= MSM_BUCKETS * MSM_SPLIT, "msm_part holds the row / column sums");
-
-__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket_sum(DevBatch B) {
-  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
-  if (j >= MSM_BUCKETS) return;
-  if (B.counters[CNT_L0_BAD]) return;
-  Jac<Fp2x> acc = px_load(B.msm_part[MSM_SPLIT * j]);
-#pragma unroll 1
-  for (uint32_t sl = 1; sl < MSM_SPLIT; ++sl) acc = jac_add_in<Fp2x, true>(acc, px_load(B.msm_part[MSM_SPLIT * j + sl]));
-  px_store(B.msm_bkt[j], acc);
-}
-
-__global__ void __launch_bounds__(2 * MSM_RC_PAIRS) k_msm_rowcol(DevBatch B) {
-  TBG_URGENT();
-  __shared__ Jac<Fp2x> lds[2 * MSM_RC_PAIRS];
-  if (B.counters[CNT_L0_BAD]) return;  // (grid-uniform)
-  const uint32_t pr = threadIdx.x >> 1, w = blockIdx.x;
-  Jac<Fp2x> acc;
-  if (w < MSM_RC_ROWS) {  // row a = w: buckets 256 a + b, two per pair
-    const uint32_t j = MSM_RC_COLS * w + 2 * pr;
-    acc = jac_add_in<Fp2x, true>(px_load(B.msm_bkt[j]), px_load(B.msm_bkt[j + 1]));
-  } else {  // column b = w - 128: buckets 256 a + b, one per pair
-    acc = px_load(B.msm_bkt[MSM_RC_COLS * pr + (w - MSM_RC_ROWS)]);
-  }
-  acc = pair_tree_sum<MSM_RC_PAIRS>(acc, lds);
-  if (pr == 0) px_store(B.msm_part[w], acc);
-}
-
-// [k] P for k < 256 (k = 0: the point at infinity)
-__device__ __forceinline__ Jac<Fp2x> px_mul_small(const Jac<Fp2x>& p, uint32_t k) {
-  if (k == 0 || jac_is_inf(p)) return jac_inf<Fp2x>();
-  Jac<Fp2x> acc = p;
-  const int top = 31 - __builtin_clz(k);
-#pragma unroll 1
-  for (int bit = top - 1; bit >= 0; --bit) {
-    acc = jac_dbl_in(acc);
-    if ((k >> bit) & 1u) acc = jac_add_in<Fp2x, true>(acc, p);
-  }
-  return acc;
-}
-
-__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_rcscale(DevBatch B) {
-  TBG_URGENT();
-  const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
-  if (w >= MSM_RC_ROWS + MSM_RC_COLS) return;
-  if (B.counters[CNT_L0_BAD]) return;
-  const uint32_t k = w < MSM_RC_ROWS ? w : w - MSM_RC_ROWS;  // a T_a, or b U_b
-  px_store(B.msm_part[MSM_RC_ROWS + MSM_RC_COLS + w], px_mul_small(px_load(B.msm_part[w]), k));
-}
-
-__global__ void __launch_bounds__(2 * MSM_RC_PAIRS) k_msm_rcfinal(DevBatch B) {
-  TBG_URGENT();
-  __shared__ Jac<Fp2x> lds[2 * MSM_RC_PAIRS];
-  if (B.counters[CNT_L0_BAD]) return;
-  const uint32_t pr = threadIdx.x >> 1;
-  const G2J* sc = B.msm_part + MSM_RC_ROWS + MSM_RC_COLS;  // scaled: rows, then columns
-  const Jac<Fp2x> z = pair_tree_sum<MSM_RC_PAIRS>(px_load(B.msm_part[pr]), lds);  // sum_a T_a
-  const Jac<Fp2x> x = pair_tree_sum<MSM_RC_PAIRS>(px_load(sc[pr]), lds);          // sum_a a T_a
-  const Jac<Fp2x> y = pair_tree_sum<MSM_RC_PAIRS>(
-      jac_add_in<Fp2x, true>(px_load(sc[MSM_RC_ROWS + pr]), px_load(sc[MSM_RC_ROWS + MSM_RC_PAIRS + pr])), lds);  // sum_b b U_b
-  if (pr != 0) return;
-  Jac<Fp2x> x512 = x;
-#pragma unroll 1
-  for (int i = 0; i < 9; ++i) x512 = jac_dbl_in(x512);
-  const Jac<Fp2x> acc = jac_add_in<Fp2x, true>(jac_add_in<Fp2x, true>(z, x512), jac_dbl_in(y));
-  if (jac_is_inf(acc)) {
-    if (pair_par() == 0) B.counters[CNT_L0_BAD] = 1;  // S = 0: no lines; the group levels decide
-    return;
-  }
-  const Fp2x zi = f_inv(acc.Z);
-  const Fp2x zi2 = f_sqr(zi);
-  px_store(*B.batch_pt, Aff<Fp2x>{f_mul(acc.X, zi2), f_mul(acc.Y, f_mul(zi2, zi))});
-}
-#endif
-
 void launch_pubkey_tables(const G1A* pk, const G1A* xpk, const int32_t* status, uint32_t n, G1A* tab, hipStream_t st) {
   if (n) TBG_KLAUNCH(k_pubkey_tables, dim3((n + BINV_BLOCK - 1) / BINV_BLOCK), dim3(BINV_BLOCK), st, pk, xpk, status, n,
                      tab);
@@ -345,16 +257,9 @@ void launch_l0_msm(const DevBatch& B, hipStream_t st) {
   TBG_KLAUNCH(k_msm_scan, dim3(1), dim3(kScanBlock), st, B);
   if (B.n_partials) TBG_KLAUNCH(k_msm_scatter, grid_for(B.n_partials), dim3(kBlock), st, B);
   TBG_KLAUNCH(k_msm_bucket_part, grid_for(2 * MSM_BUCKETS * MSM_SPLIT), dim3(kBlock), st, B);
-#if TBG_MSM_RC
-  TBG_KLAUNCH(k_msm_bucket_sum, grid_for(2 * MSM_BUCKETS), dim3(kBlock), st, B);
-  TBG_KLAUNCH(k_msm_rowcol, dim3(MSM_RC_ROWS + MSM_RC_COLS), dim3(2 * MSM_RC_PAIRS), st, B);
-  TBG_KLAUNCH(k_msm_rcscale, grid_for(2 * (MSM_RC_ROWS + MSM_RC_COLS)), dim3(kBlock), st, B);
-  TBG_KLAUNCH(k_msm_rcfinal, dim3(1), dim3(2 * MSM_RC_PAIRS), st, B);
-#else
   TBG_KLAUNCH(k_msm_bucket, grid_for(2 * MSM_BUCKETS), dim3(kBlock), st, B);
   TBG_KLAUNCH(k_msm_tree, dim3(MSM_TREE_WG), dim3(2 * MSM_TREE_PAIRS), st, B);
   TBG_KLAUNCH(k_msm_tree_final, dim3(1), dim3(MSM_TREE_WG), st, B);
-#endif
 }
 
 }  // namespace tbg

@@ -17,11 +17,6 @@ constexpr int kBlock = 64;
 // need more than one round of the device's wave slots picks (G, C) among
 // (16, 4), (16, 8), (14, 7) by rounds x hexad length (tbls_engine.hip,
 // l0_shape); 0: always (16, 4).
-// Level 0's bucket scalings: 1 = by row and column sums (k_msm.hip
-// k_msm_rowcol: 384 small scalings), 0 = one 16-bit scaling per bucket
-#ifndef TBG_MSM_RC
-#define TBG_MSM_RC 1
-#endif
 // Per-key G1 tables for the RLC products [r_i] pk_i: 1 = the 8-entry window
 // table (bls_rlc.h rlc_mul_key_w2: 14 doublings + 16 additions), 0 = the
 // 2-entry pair table pk +- [x]pk (15 + 32)
