@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-5 call: parity / headline / config-2 oracle / replay GPU tests with
+# level 0's bucket scalings by row and column sums (TBG_MSM_RC), then A/B
+# against one scaling per bucket (rc0): driver shape twice, 48 steps,
+# config 3.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+bash tools/gpu_r04_tests.sh r5t13 "tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_fullsize.py::test_config2_full_batch_matches_oracle tests/test_gpu_replay_shape.py tests/test_gpu_shape.py" || exit 1
+O=$R/gpurun_out/r5rc
+mkdir -p $O
+run() {  # lib name args...
+  local l=$1 n=$2 f=$O/$2.json; shift 2
+  if [ "$l" = product ]; then unset TBG_LIB; else export TBG_LIB=$R/$l; fi
+  timeout -k 10 300 python3 -u bench.py --no-cpu --api-batches 0 --latency 0 "$@" > $f 2> $f.err || { tail -20 $f.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$f'));k=d['isolated_kernel_ms'];print('$n', d['value'], d['ms_per_step'], d['config']['level0'], {x: k[x] for x in k if 'msm' in x})"
+}
+for rep in 1 2; do
+  run product p_s20_$rep --steps 20 --warmup 5 || exit 1
+  run varlib/rc0.so c_s20_$rep --steps 20 --warmup 5 || exit 1
+done
+run product p_s48 --steps 48 --warmup 5 || exit 1
+run varlib/rc0.so c_s48 --steps 48 --warmup 5 || exit 1
+run product p_c3 --workload config3 --steps 6 --warmup 2 || exit 1
+run varlib/rc0.so c_c3 --workload config3 --steps 6 --warmup 2 || exit 1
+unset TBG_LIB
