@@ -17,7 +17,7 @@
 // them.  Each Q_k is a bucket sum: bucket (k, v) adds +-s_i over the members
 // with |c_ik| = v, and Q_k = sum_v v B_(k,v) by running sums -- ~16.6 mixed
 // additions per signature instead of ~68 group operations, plus 18 tests per
-// group of 512.
+// group of 1,024.
 //
 //   k_sgb_sort    one workgroup per group: digits, bucket counts and entries in LDS
 //   k_sgb_bucket  one lane PAIR per (group, bucket, slice): the slice's sum

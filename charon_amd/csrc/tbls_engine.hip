@@ -692,7 +692,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_bf = sec(l0 ? 4ull * 3 * 4 * NL : 0);
   size_t w_gf = sec(l0 ? 4ull * 3 * 4 * NL * grp_f_entries(ng) : 0);
   // Batched subgroup test while the collected batches carry (almost) no
-  // non-subgroup signature: groups of 512 partials, a failed group's members
+  // non-subgroup signature: groups of 1,024 partials, a failed group's members
   // tested alone (k_sgb.hip); small batches test every signature alone.
   const bool sgb = np >= SGB_MIN_PARTIALS &&
                    (c->sgb_mode == TBG_SGB_ON || (c->sgb_mode == TBG_SGB_AUTO && c->nonsub_ema < TBG_SGB_AUTO_MAX));

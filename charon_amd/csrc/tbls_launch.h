@@ -186,7 +186,7 @@ constexpr uint32_t MSM_SUM_ENTRIES = 128;
 // combination hides such a component with probability <= 1/13, so SGB_K =
 // 18 independent combinations leave 13^-18 < 2^-66.
 #ifndef TBG_SGB_M
-#define TBG_SGB_M 512
+#define TBG_SGB_M 1024
 #endif
 #ifndef TBG_SGB_SPLIT
 #define TBG_SGB_SPLIT 4
@@ -195,7 +195,7 @@ constexpr uint32_t SGB_M = TBG_SGB_M;  // consecutive partials per group
 constexpr uint32_t SGB_K = 18;         // combinations per group
 constexpr uint32_t SGB_V = 6;          // buckets per combination (|c| = 1..6)
 constexpr uint32_t SGB_BUCKETS = SGB_K * SGB_V;
-constexpr uint32_t SGB_SPLIT = TBG_SGB_SPLIT;  // slices per bucket (~20 additions each at SGB_M = 512)
+constexpr uint32_t SGB_SPLIT = TBG_SGB_SPLIT;  // slices per bucket (~40 additions each at SGB_M = 1024)
 constexpr uint32_t SGB_MIN_PARTIALS = 2 * SGB_M;  // smaller batches test each signature alone
 TBG_HD inline uint32_t sgb_groups(uint32_t n_partials) { return (n_partials + SGB_M - 1) / SGB_M; }
 // Level-0 product tree over the groups' P-chunk products.  Each pass is a

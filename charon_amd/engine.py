@@ -249,7 +249,7 @@ class Engine:
 
     def subgroup(self, ticket) -> dict:
         """Batched subgroup test of the batch's last run (tbg_fetch_subgroup):
-        groups of 512 partials tested by random combinations (0: every
+        groups of 1,024 partials tested by random combinations (0: every
         signature tested alone) and how many failed."""
         out = np.zeros(2, dtype=np.uint32)
         self._check(self._lib.tbg_fetch_subgroup(self._h, ticket, _ptr(out)), "tbg_fetch_subgroup")

@@ -106,10 +106,10 @@ typedef struct {
                            * longer lists run in several passes                       */
   uint32_t subgroup_batch; /* G2 subgroup checks of the decoded signatures:
                            * TBG_SGB_AUTO (0) random-combination tests per group of
-                           * 512 partials, each member tested alone only when its
+                           * 1,024 partials, each member tested alone only when its
                            * group fails, while the non-subgroup share average is
                            * below TBG_SGB_AUTO_MAX; TBG_SGB_ON always; TBG_SGB_OFF
-                           * every signature alone.  Batches below 1024 partials
+                           * every signature alone.  Batches below 2,048 partials
                            * always test each signature alone.                        */
   uint32_t express_partials; /* batches of at most this many partials go to an extra
                            * slot on a high-priority stream when it is free (a small
@@ -122,8 +122,8 @@ typedef struct {
 #define TBG_SGB_AUTO 0
 #define TBG_SGB_ON 1
 #define TBG_SGB_OFF 2
-/* (with 512 partials per group ~10 % of the groups fail at this share: the
- * batched test then costs ~0.6 of testing every signature alone) */
+/* (with 1,024 partials per group ~18 % of the groups fail at this share: the
+ * batched test then costs ~0.7 of testing every signature alone) */
 #define TBG_SGB_AUTO_MAX 2e-4
 #define TBG_GIDENT_OFF 0
 #define TBG_GIDENT_L3 1
@@ -256,7 +256,7 @@ int tbg_fetch_level0(tbg_ctx* ctx, tbg_ticket ticket, int32_t* state);
  * duties per group, level 0 (TBG_L0_*)]. */
 int tbg_fetch_fallback(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out8);
 /* Batched subgroup test of a collected batch's last run (tbg_config.
- * subgroup_batch): out2 = [groups of 512 partials tested by random
+ * subgroup_batch): out2 = [groups of 1,024 partials tested by random
  * combinations (0: every signature was tested alone), groups that failed
  * (their members were then tested one by one)]. */
 int tbg_fetch_subgroup(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out2);

@@ -3,7 +3,7 @@
 Signatures crafted against random combinations (tests/golden/sgb_points.json:
 13- and 23-torsion components, a bare torsion point, a pair whose components
 cancel in a plain sum) and a random non-subgroup point are placed at the
-first and last position of a group of 512 partials, two in one group, the
+first and last position of a group of 1,024 partials, two in one group, the
 cancelling pair in one group, and the last partial of a short final group.
 Every partial's status, every duty status and every aggregate must equal
 oracle/c's per-item schedule (tblsconv.SigFromCore's subgroup check,
@@ -19,14 +19,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-M = 512  # SGB_M
+M = 1024  # SGB_M
 
 
 def crafted_batch(engine):
     from tools.workload import invalid_pool, make_batch
     with open(os.path.join(HERE, "golden", "sgb_points.json")) as f:
         pts = {k: [bytes.fromhex(h) for h in v] for k, v in json.load(f)["points"].items()}
-    b = make_batch(engine, 1500, 3, 4, seed=4242)  # 6000 partials: 11 full groups + one of 368
+    b = make_batch(engine, 1500, 3, 4, seed=4242)  # 6000 partials: 5 full groups + one of 880
     n_p = len(b.sigs)
     place = {
         0: pts["t13"][0],                      # group 0, first member

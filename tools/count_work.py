@@ -138,13 +138,13 @@ def main():
     duty_sum4 -= saved
     rlc_partial -= saved  # (k_rlc_partial2: the n2 inversion batched; its G1 product now from the key's table)
     hash_ -= 2 * saved
-    # batched subgroup test (k_sgb.hip, SGB_M = 512, 18 combinations with
+    # batched subgroup test (k_sgb.hip, SGB_M = 1024, 18 combinations with
     # digits uniform mod 13: 12/13 of them non-zero): per partial 18 * 12 / 13
     # mixed additions into buckets; per group and combination the running
     # sums over 6 buckets x 4 slices (30 additions) and one psi(Q) == [x]Q
     # test on a Jacobian Q (the affine test with its 5 mixed additions full)
     madd, _ = measure(lib.hc_k_msm_entry, 0)  # k = 0: psi^0, one mixed addition
-    sgb_m, sgb_k = 512, 18
+    sgb_m, sgb_k = 1024, 18
     sgb_bucket = sgb_k * 12 / 13 * madd
     sgb_fold = sgb_k * 6 * 3 * g2_add / sgb_m  # each bucket's 4 slices into one
     sgb_combine = sgb_k * 12 * g2_add / sgb_m  # the running sums over the 6 folded buckets
