@@ -72,8 +72,8 @@ def test_crafted_points_match_oracle_batched_and_alone(engines):
     assert_same(res, ref)
     assert np.flatnonzero(res.partial_status == eng.PS_ERR_SUBGROUP).tolist() == bad
     n_sg = (len(b.sigs) + M - 1) // M
-    # groups 0, 1, 2, 5 and the last failed; every other group passed whole
-    assert sg == {"groups": n_sg, "failed": 5}, sg
+    # the groups holding a crafted point failed; every other group passed whole
+    assert sg == {"groups": n_sg, "failed": len({i // M for i in bad})}, sg
     # the same batch with every signature tested alone: identical results
     b2, _ = crafted_batch(e_off)
     res2, sg2 = run(e_off, b2)
@@ -88,7 +88,7 @@ def test_adaptive_mode_turns_off_and_on(engines):
     e = engines[eng.SGB_AUTO]
     b, bad = crafted_batch(e)
     res, sg = run(e, b)  # first batch: clean history, batched
-    assert sg["groups"] > 0 and sg["failed"] == 5
+    assert sg["groups"] > 0 and sg["failed"] == len({i // M for i in bad})
     assert np.flatnonzero(res.partial_status == eng.PS_ERR_SUBGROUP).tolist() == bad
     # 8 / 6000 non-subgroup partials: the average passes TBG_SGB_AUTO_MAX, the next batch tests alone
     clean = make_batch(e, 1500, 3, 4, seed=4343)
