@@ -10,7 +10,9 @@ no cross-GPU math; BASELINE config 4 is this at 125k DVs per GPU).
 
 Single GPU:  python bench.py
 N GPUs:      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-Prints one JSON line (rank 0).
+             or python bench.py --gpus N (starts the N rank processes itself)
+Ranks meet on gloo (barrier + max over ranks); each holds one HIP runtime,
+the engine library's.  Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -59,27 +61,88 @@ PEAK_MAD_TOPS = 32.8
 PEAK_MAD_TOPS_CLOCK = 39.3
 
 
+def rank_env():
+    """(world size, rank, local rank) from the launcher's environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+_JSON_FD = None
+
+
+def emit(obj) -> None:
+    """Print the one JSON line (rank 0) on the process's original stdout."""
+    line = (json.dumps(obj) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
+def quiet_stdout() -> None:
+    """Keep stdout for the JSON line alone: everything else the process
+    writes to fd 1 (gloo's C++ connection messages among it) goes to stderr."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
 def dist_setup():
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    """Join the rank group on gloo (CPU).  The ranks exchange only a barrier
+    and the max of their elapsed times -- no data-path collective (DV-duties
+    shard with no cross-GPU math) -- so nothing here touches the
+    GPU: torch is imported for torch.distributed only, after the engine
+    library holds the process's one HIP runtime."""
+    ws, rank, local = rank_env()
     if ws > 1:
+        quiet_stdout()
         import torch.distributed as dist
-        backend = os.environ.get("TBG_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            import torch
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+        dist.init_process_group(backend="gloo")
     return ws, rank, local
 
 
-def barrier_sync(ws):
-    try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-    except Exception:
-        pass
+def launch_ranks(n: int, argv) -> int:
+    """`--gpus N` without a launcher (WORLD_SIZE unset): start N fresh rank
+    processes of this script, one per GPU (LOCAL_RANK = rank), with the
+    environment torch.distributed.run would give them, before this process
+    touches the GPU; wait for all of them and return the first failure's exit
+    code (the others are stopped).  Rank 0 prints the JSON line."""
+    import signal
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+    return rc
+
+
+def barrier_sync(ws, sync=None):
+    """Device synchronisation (the engine's streams) then the rank barrier;
+    errors propagate."""
+    if sync is not None:
+        sync()
     if ws > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -90,20 +153,42 @@ def max_over_ranks(x: float, ws: int) -> float:
         return x
     import torch
     import torch.distributed as dist
-    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def timed_steps(step_fn, steps: int, ws: int):
+def timed_steps(step_fn, steps: int, ws: int, sync=None):
     """Barrier + sync on both sides of exactly `steps` steps; max over ranks."""
-    barrier_sync(ws)
+    barrier_sync(ws, sync)
     t0 = time.perf_counter()
     out = step_fn(steps)
-    barrier_sync(ws)
+    barrier_sync(ws, sync)
     dt = time.perf_counter() - t0
     return max_over_ranks(dt, ws), out
+
+
+def launch_check(args):
+    """--launch-check: the rank plumbing alone (no engine, no GPU): every rank
+    joins the gloo group, runs a timed region of rank-dependent length, and
+    rank 0 prints the ranks it saw with the max-over-ranks time."""
+    ws, rank, local = dist_setup()
+
+    def step(k):
+        time.sleep(0.05 * (rank + 1) * k)
+        return k
+
+    dt, _ = timed_steps(step, args.steps, ws)
+    seen = [(rank, local, os.getpid())]
+    if ws > 1:
+        import torch.distributed as dist
+        allv = [None] * ws
+        dist.all_gather_object(allv, seen[0])
+        seen = allv
+        dist.destroy_process_group()
+    if rank == 0:
+        emit({"launch_check": True, "n_gpus": ws, "ranks": [list(x) for x in seen],
+                          "elapsed_max_s": round(dt, 4)})
 
 
 def work_model():
@@ -422,11 +507,10 @@ def config4_multi(args):
     one-GPU box eight contexts share it), gathered into caller order by
     tbg_multi_collect.  Host packing, H2D, the chains and D2H are all inside
     the clock (the product path, not HBM-resident); every result is checked."""
-    import torch
     from charon_amd import engine as eng
     from tools.workload import make_mixed_batch
     from charon_amd.shard import sub_batch
-    ndev = max(1, torch.cuda.device_count())
+    ndev = max(1, eng.device_count())
     devs = [i % ndev for i in range(args.multi_contexts)]
     m = eng.MultiEngine(devs, slots=1)
     try:
@@ -490,7 +574,11 @@ WORKLOADS = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one GPU each (default: WORLD_SIZE, else 1).  Without a launcher (WORLD_SIZE "
+                         "unset) N > 1 starts N rank processes itself; under one, N must equal WORLD_SIZE")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="run only the rank plumbing (gloo barrier, max-over-ranks) and print the ranks seen")
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--dvs", type=int, default=10000)
@@ -534,12 +622,25 @@ def main():
                     help="batches pushed through the product path (tbg_submit / tbg_collect, host packing and PCIe "
                          "included) for the api_pipeline side key; 0 skips it")
     args = ap.parse_args()
+    ws_env = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(ws_env) if ws_env else 1
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if ws_env is None and args.gpus > 1:
+        # no launcher: this process only starts the ranks (it never touches the GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if ws_env is not None and int(ws_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws_env} ranks were launched")
+    if args.launch_check:
+        launch_check(args)
+        return
     if args.workload == "config4" and args.multi_contexts:
-        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        if args.gpus != 1:
             sys.exit("bench.py: --multi-contexts drives every GPU from one process (no torch.distributed launch)")
         args.dvs = 1_000_000 if args.dvs == 10000 else args.dvs
         args.inject = 0.0 if args.inject is None else args.inject
-        print(json.dumps(config4_multi(args)))
+        emit(config4_multi(args))
         return
     if args.workload == "config4":
         args.dvs, args.t, args.n = 125000, 3, 4
@@ -552,14 +653,18 @@ def main():
     if args.workload != "config2":
         args.api_batches = 0  # the product-path side key is measured on the headline shape
 
-    ws, rank, local = dist_setup()
+    # The engine library is loaded first: its HIP runtime (ROCm's
+    # libamdhip64.so.7) is the one the process initialises; torch comes in
+    # afterwards for torch.distributed on gloo only and never touches the GPU.
     from charon_amd import engine as eng
     from tools.workload import make_batch, make_mixed_batch
-
-    # one GPU per rank (LOCAL_RANK); modulo the visible count so a gloo
-    # rehearsal of N ranks can share one card (identity on an 8-GPU node)
-    import torch
-    device = local % max(1, torch.cuda.device_count())
+    ndev = eng.device_count()
+    if ndev < 1:
+        sys.exit("bench.py: no HIP device visible to the engine")
+    ws, rank, local = dist_setup()
+    # one GPU per rank (LOCAL_RANK); modulo the visible count so N ranks can
+    # share one card on a one-GPU box (identity on an 8-GPU node)
+    device = local % ndev
     # one slot more than the replayed launches: the product-path side key packs
     # the next group into it while `inflight` launches run (the replay uses
     # only the first `inflight` slots)
@@ -628,16 +733,25 @@ def main():
     def step_fn(k):
         kernel_ms.update(e.replay_plan(*plan(k)))
 
-    elapsed, _ = timed_steps(step_fn, args.steps, ws)
+    elapsed, _ = timed_steps(step_fn, args.steps, ws, sync=e.synchronize)
     # outputs of the timed replays must still be exact (every batch of every slot)
+    exact_after = True
     for group, t0 in zip(batches, tickets):
         for k, b in enumerate(group):
             again = e.fetch(t0 + k, b.n_dv, len(b.identifiers))
-            assert batch_exact(again, b, eng)
+            exact_after = exact_after and batch_exact(again, b, eng)
+    if ws > 1:  # every rank's re-check, reported by rank 0
+        import torch.distributed as dist
+        allx = [None] * ws
+        dist.all_gather_object(allx, {"rank": rank, "device": device, "exact": bool(exact_after)})
+    else:
+        allx = [{"rank": 0, "device": device, "exact": bool(exact_after)}]
+    if not all(x["exact"] for x in allx):
+        print(json.dumps({"error": "timed replays' outputs differ", "ranks": allx}), file=sys.stderr)
+        sys.exit(3)
     b = batches[0][0]
     flat = [x for g in batches for x in g]
     group_used = e.stats(tickets[0])["group_size"]  # before api_pipeline reuses the slots (tickets expire)
-    shape = e.shape(tickets[0])
     l0_state = e.level0(tickets[0])
     fallback = e.fallback(tickets[0])  # per-level fallback work of the slot's last run
     slot_dev, slot_pinned = e.slot_bytes(tickets[0])
@@ -651,6 +765,7 @@ def main():
     # replayed alone, an event pair around every kernel -- the exclusive
     # durations the roofline prices; the stage sums are isolated_batch_ms.
     kp = kernel_profile(e.replay_profile(tickets[0]))
+    shape = e.shape(tickets[0])  # the shape that profiled replay ran (the whole device batch)
     iso = {st: round(sum(kp[k][0] for k in ks if k in kp), 3) for st, ks in STAGE_KERNELS.items()}
     iso["total"] = round(sum(v[0] for v in kp.values()), 3)
     wm = work_model()
@@ -677,6 +792,7 @@ def main():
                    "rlc_group": group_used, "rlc_chunk": shape["chunk"], "gident": args.gident, "subgroup_batch": args.subgroup_batch,
                    "level0": {eng.L0_NOT_RUN: "not run", eng.L0_PASSED: "passed", eng.L0_FAILED: "failed"}[l0_state],
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
+        "ranks_exact_after_clock": allx,
         "fallback_levels": fallback,
         "subgroup_batch": subgroup,
         "slot_bytes": {"device": int(slot_dev), "pinned_host": int(slot_pinned), "batches_per_slot": M},
@@ -700,7 +816,7 @@ def main():
     if rank == 0 and not args.no_cpu and ws == 1 and args.workload in ("config2", "config3", "config4"):
         result["cpu_baseline"] = cpu_baseline(b, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(result))
+        emit(result)
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -194,6 +194,8 @@ SIGNATURES = {
     "tbg_destroy": (None, [ctypes.c_void_p]),
     "tbg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "tbg_device_count": (ctypes.c_int, []),
+    "tbg_device_cu_count": (ctypes.c_int, [ctypes.c_int]),
+    "tbg_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "tbg_load_pubkeys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                         ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p]),
     "tbg_pubkey_count": (ctypes.c_uint32, [ctypes.c_void_p]),

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(kSgbSortBlock) k_sgb_sort(DevBatch B) {
   for (uint32_t li = t; li < n; li += kSgbSortBlock) {
     const bool ok = B.partial_status[i0 + li] == TBG_PS_NOT_VERIFIED;
     int32_t c[SGB_K];
-    sgb_digits(B.rlc_seed, i0 + li, c);
+    sgb_digits(B.sgb_seed, i0 + li, c);
 #pragma unroll
     for (uint32_t k = 0; k < SGB_K; ++k) {
       const int32_t d = ok ? c[k] : 0;

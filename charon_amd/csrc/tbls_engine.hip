@@ -100,6 +100,8 @@ struct Slot {
   uint64_t seen_bad = 0, seen_total = 0;  // invalid / verified partials of the parts collected so far
   uint64_t seen_nsub = 0, seen_dec = 0;   // non-subgroup / all partials of the parts collected so far
   tbg::DevBatch B{};           // device view of the last batch (resident until the slot is reused)
+  tbg::DevBatch last{};        // the batch as its last run launched it (a replay's prefix and shape):
+                               // what tbg_fetch_stats / _fallback / _shape / _subgroup describe
   size_t w_out = 0;
 };
 
@@ -198,6 +200,27 @@ int tbg_device_count(void) {
   return n;
 }
 
+int tbg_device_cu_count(int device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return TBG_E_NO_DEVICE;
+  if (device < 0 || device >= ndev) return TBG_E_INVALID_ARG;
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return TBG_E_DEVICE;
+  return n_cu;
+}
+
+int tbg_synchronize(tbg_ctx* c) {
+  if (!c) return TBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto& s : c->slots) {
+    if (s.st) HIP_TRY(hipStreamSynchronize(s.st));
+    if (s.st2 && s.st2 != s.st) HIP_TRY(hipStreamSynchronize(s.st2));
+  }
+  return TBG_OK;
+}
+
 int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   if (!out) return TBG_E_INVALID_ARG;
   *out = nullptr;
@@ -242,6 +265,9 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out) {
   // other leaves idle).
   uint32_t nslots = (cfg && cfg->slots) ? cfg->slots : 3;
   const uint32_t spp = (cfg && cfg->streams_per_slot > 1) ? cfg->streams_per_slot : 1;
+  // The express slot takes one stream more; a configuration with no stream
+  // left for it runs without one rather than being refused.
+  if (nslots * spp + 1 > TBG_MAX_SLOT_STREAMS) c->express_max = TBG_EXPRESS_OFF;
   const bool express = c->express_max != TBG_EXPRESS_OFF;
   if (nslots > TBG_MAX_SLOTS || spp > 2 || nslots * spp + (express ? 1 : 0) > TBG_MAX_SLOT_STREAMS) {
     hipStreamDestroy(c->stream);
@@ -577,8 +603,13 @@ static void l0_shape(uint64_t nd, uint32_t n_simd, bool g_free, uint32_t& G, uin
 static bool l0_shape_fits(uint32_t nd0, uint32_t G0, uint32_t C0, uint32_t nd, uint32_t G, uint32_t C) {
   const uint64_t ng0 = (nd0 + G0 - 1) / G0, nch0 = (G0 + C0 - 1) / C0;
   const uint64_t ng = (nd + G - 1) / G, nch = (G + C - 1) / C;
-  return ng <= ng0 && ng * (nch + 1) <= ng0 * (nch0 + 1) && ng * nch * C <= ng0 * nch0 * C0 && ng * G <= ng0 * G0 &&
-         std::max(ng * nch, (uint64_t)nd) <= std::max(ng0 * nch0, (uint64_t)nd0) && (G <= 64) == (G0 <= 64);
+  // every group / chunk section of the arena (tbg_submit_group's w_cf,
+  // w_gidf: ng (nch + 1); w_cl, w_cfe, w_cidl: ng nch -- ADVICE r05: the
+  // max() below alone let nd0 hide an overflow of these; w_cidp: ng nch C;
+  // w_gidp: ng G; w_pend: max(ng nch, nd); grp_f: ng)
+  return ng <= ng0 && ng * (nch + 1) <= ng0 * (nch0 + 1) && ng * nch <= ng0 * nch0 && ng * nch * C <= ng0 * nch0 * C0 &&
+         ng * G <= ng0 * G0 && std::max(ng * nch, (uint64_t)nd) <= std::max(ng0 * nch0, (uint64_t)nd0) &&
+         (G <= 64) == (G0 <= 64);
 }
 
 int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches, tbg_ticket* tickets) {
@@ -838,6 +869,10 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
       B.rlc_seed[2 * j] = (uint32_t)(k[j] >> 32);
       B.rlc_seed[2 * j + 1] = (uint32_t)k[j];
     }
+    // The batched subgroup test's key never follows rlc_seed:
+    // its soundness needs coefficients a submitter cannot predict.
+    std::random_device rd;
+    for (auto& w : B.sgb_seed) w = rd() ^ (uint32_t)(++c->seed_ctr * 0x9E3779B9u);
   }
   B.rlc_chunk = C;
   B.part_p = (G1J*)(dw + w_pp);
@@ -933,6 +968,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   s->n_msgs = nm;
   s->out_bytes = out_bytes;
   s->B = B;
+  s->last = B;
   s->w_out = w_out;
   return TBG_OK;
 }
@@ -1094,6 +1130,7 @@ int tbg_replay_plan(tbg_ctx* c, const tbg_ticket* tickets, const uint32_t* n_par
     for (int stage = 0; stage < 3 && rc == TBG_OK; ++stage)
       for (uint32_t k = k0; k < k1 && rc == TBG_OK; ++k)
         rc = launch_chain(c, *sl[k], bs[k], ev.data() + (size_t)kChainEvents * k, stage);
+    for (uint32_t k = k0; k < k1; ++k) sl[k]->last = bs[k];
     k0 = k1;
   }
   for (uint32_t k = 0; k < n_launches; ++k) {
@@ -1136,6 +1173,7 @@ int tbg_replay_profile(tbg_ctx* c, tbg_ticket t, tbg_kernel_time* out, uint32_t 
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
   g_kprof = &rec;
   int rc = launch_chain(c, *s, s->B, ev);
+  s->last = s->B;
   g_kprof = nullptr;
   if (hipStreamSynchronize(s->st) != hipSuccess || hipStreamSynchronize(s->st2) != hipSuccess) rc = TBG_E_DEVICE;
   uint32_t n = 0;
@@ -1185,14 +1223,14 @@ int tbg_fetch_stats(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
   HIP_TRY(hipSetDevice(c->device));
   uint32_t cnt[CNT_WORDS] = {};
   if (s->op != TBG_OP_AGGREGATE) {
-    HIP_TRY(hipMemcpyAsync(cnt, s->B.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
+    HIP_TRY(hipMemcpyAsync(cnt, s->last.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
     HIP_TRY(hipStreamSynchronize(s->st));
   }
-  uint32_t ng = s->B.rlc_group ? (s->n_duties + s->B.rlc_group - 1) / s->B.rlc_group : 0;
+  uint32_t ng = s->last.rlc_group ? (s->last.n_duties + s->last.rlc_group - 1) / s->last.rlc_group : 0;
   out4[0] = ng;
   out4[1] = cnt[CNT_DUTIES];
   out4[2] = cnt[CNT_PARTIALS];
-  out4[3] = s->B.rlc_group;
+  out4[3] = s->last.rlc_group;
   return TBG_OK;
 }
 
@@ -1204,17 +1242,17 @@ int tbg_fetch_fallback(tbg_ctx* c, tbg_ticket t, uint32_t* out8) {
   HIP_TRY(hipSetDevice(c->device));
   uint32_t cnt[CNT_WORDS] = {};
   if (s->op != TBG_OP_AGGREGATE) {
-    HIP_TRY(hipMemcpyAsync(cnt, s->B.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
+    HIP_TRY(hipMemcpyAsync(cnt, s->last.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
     HIP_TRY(hipStreamSynchronize(s->st));
   }
-  out8[0] = s->B.rlc_group ? (s->n_duties + s->B.rlc_group - 1) / s->B.rlc_group : 0;
+  out8[0] = s->last.rlc_group ? (s->last.n_duties + s->last.rlc_group - 1) / s->last.rlc_group : 0;
   out8[1] = cnt[CNT_GID];
   out8[2] = cnt[CNT_CHUNKS];
   out8[3] = cnt[CNT_CID];
   out8[4] = cnt[CNT_DUTIES];
   out8[5] = cnt[CNT_PARTIALS];
-  out8[6] = s->B.rlc_group;
-  out8[7] = s->op == TBG_OP_AGGREGATE || !s->B.rlc_batch ? (uint32_t)TBG_L0_NOT_RUN
+  out8[6] = s->last.rlc_group;
+  out8[7] = s->op == TBG_OP_AGGREGATE || !s->last.rlc_batch ? (uint32_t)TBG_L0_NOT_RUN
             : cnt[CNT_L0_OK]                              ? (uint32_t)TBG_L0_PASSED
                                                           : (uint32_t)TBG_L0_FAILED;
   return TBG_OK;
@@ -1225,11 +1263,11 @@ int tbg_fetch_shape(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
   std::lock_guard<std::mutex> lk(c->mu);
   Slot* s = find_ticket(c, t, false, nullptr);
   if (!s) return TBG_E_TICKET;
-  const uint32_t G = s->B.rlc_group, C = s->B.rlc_chunk;
+  const uint32_t G = s->last.rlc_group, C = s->last.rlc_chunk;
   out4[0] = G;
   out4[1] = G ? C : 0;
-  out4[2] = s->B.rlc_batch ? 1u : 0u;
-  out4[3] = G ? ((s->n_duties + G - 1) / G) * ((G + C - 1) / C) : 0;
+  out4[2] = s->last.rlc_batch ? 1u : 0u;
+  out4[3] = G ? ((s->last.n_duties + G - 1) / G) * ((G + C - 1) / C) : 0;
   return TBG_OK;
 }
 
@@ -1240,10 +1278,10 @@ int tbg_fetch_subgroup(tbg_ctx* c, tbg_ticket t, uint32_t* out2) {
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
   out2[0] = out2[1] = 0;
-  if (!s->B.sgb) return TBG_OK;
-  const uint32_t n_sg = sgb_groups(s->n_partials);
+  if (!s->last.sgb) return TBG_OK;
+  const uint32_t n_sg = sgb_groups(s->last.n_partials);
   std::vector<uint32_t> bad(n_sg);
-  HIP_TRY(hipMemcpyAsync(bad.data(), s->B.sgb_bad, 4ull * n_sg, hipMemcpyDeviceToHost, s->st));
+  HIP_TRY(hipMemcpyAsync(bad.data(), s->last.sgb_bad, 4ull * n_sg, hipMemcpyDeviceToHost, s->st));
   HIP_TRY(hipStreamSynchronize(s->st));
   out2[0] = n_sg;
   for (uint32_t g = 0; g < n_sg; ++g) out2[1] += bad[g] ? 1u : 0u;
@@ -1272,10 +1310,10 @@ int tbg_fetch_level0(tbg_ctx* c, tbg_ticket t, int32_t* state) {
   Slot* s = find_ticket(c, t, false, nullptr);
   if (!s) return TBG_E_TICKET;
   *state = TBG_L0_NOT_RUN;
-  if (s->op == TBG_OP_AGGREGATE || !s->B.rlc_batch) return TBG_OK;
+  if (s->op == TBG_OP_AGGREGATE || !s->last.rlc_batch) return TBG_OK;
   HIP_TRY(hipSetDevice(c->device));
   uint32_t cnt[CNT_WORDS] = {};
-  HIP_TRY(hipMemcpyAsync(cnt, s->B.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
+  HIP_TRY(hipMemcpyAsync(cnt, s->last.counters, sizeof(cnt), hipMemcpyDeviceToHost, s->st));
   HIP_TRY(hipStreamSynchronize(s->st));
   *state = cnt[CNT_L0_OK] ? TBG_L0_PASSED : TBG_L0_FAILED;
   return TBG_OK;

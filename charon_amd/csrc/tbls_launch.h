@@ -153,6 +153,9 @@ struct DevBatch {
   // c_i uniform mod 13 are tested psi(Q) == [x] Q; only the members of a
   // failed group take the per-signature test (k_subgroup_sigs)
   uint32_t sgb;           // 1: the batched test runs (0: every signature is tested alone)
+  uint32_t sgb_seed[8];   // secret per-batch key of the combinations' digits: always fresh OS
+                          // entropy, even under a fixed rlc_seed (a predictable key would let a
+                          // submitter craft torsion components that cancel across combinations)
   uint32_t* sgb_off;      // [n_sg][SGB_BUCKETS + 1] bucket offsets into the group's entries
   uint32_t* sgb_ent;      // [n_sg][SGB_M * SGB_K] entries: member << 1 | negative
   G2J* sgb_part;          // [n_sg][SGB_BUCKETS][SGB_SPLIT] bucket slice sums

@@ -74,6 +74,21 @@ class BatchResult:
 _serial = itertools.count(1)
 
 
+def device_count() -> int:
+    """HIP devices visible to the engine library (tbg_device_count)."""
+    return int(_native.load().tbg_device_count())
+
+
+def device_cu_count(device: int = 0) -> int:
+    """Compute units of a device, asked through the engine's own HIP runtime
+    (tbg_device_cu_count) -- not torch.cuda, whose bundled runtime would be a
+    second one in the process."""
+    n = int(_native.load().tbg_device_cu_count(device))
+    if n <= 0:
+        raise EngineError(f"tbg_device_cu_count({device}): {_native.load().tbg_strerror(n).decode()} ({n})")
+    return n
+
+
 class Engine:
     """One context = one GPU (HIP device ordinal)."""
 
@@ -188,6 +203,10 @@ class Engine:
             return False
         self._check(rc, "tbg_poll")
         return True
+
+    def synchronize(self):
+        """Wait for every stream of this context (tbg_synchronize)."""
+        self._check(self._lib.tbg_synchronize(self._h), "tbg_synchronize")
 
     def replay(self, ticket, iters=1):
         """Re-run a collected batch's kernel chain on its resident inputs."""

@@ -75,6 +75,9 @@ typedef uint64_t tbg_ticket;
  * HSA runtime runs out of queue resources (observed on MI355X).  tbg_init
  * refuses slots > TBG_MAX_SLOTS and slots * streams_per_slot >
  * TBG_MAX_SLOT_STREAMS with TBG_E_INVALID_ARG instead of failing inside HIP.
+ * The express slot (express_partials) owns one stream more: when
+ * slots * streams_per_slot + 1 would pass the bound, the context runs
+ * without an express slot instead.
  * The bound is per context: several contexts on ONE device (tbg_multi_init
  * with a repeated ordinal) add their streams up, so keep their sum below it. */
 #define TBG_MAX_SLOTS 12
@@ -90,7 +93,9 @@ typedef struct {
   uint32_t rlc_group;     /* duties per level-1 RLC group; 0 -> adaptive: 16 while the
                            * collected batches are clean, 8 / 4 once their share of
                            * invalid partials passes 0.3 % / 3 % (TBG_RLC_AUTO_*)   */
-  uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests) */
+  uint64_t rlc_seed;      /* 0: fresh OS randomness per batch; else fixed (tests).
+                           * Keys the RLC scalars only: the batched subgroup test's
+                           * combinations always take fresh OS randomness            */
   uint32_t rlc_chunk;     /* duties per Miller-loop quad inside a group (0 -> 4)  */
   uint32_t streams_per_slot; /* 1 (0 -> 1) or 2: hash_to_G2 on its own stream   */
   uint32_t rlc_batch;     /* level 0, the whole device batch as ONE check (RLC mode):
@@ -179,6 +184,14 @@ int tbg_init(const tbg_config* cfg, tbg_ctx** out);
 void tbg_destroy(tbg_ctx* ctx);
 const char* tbg_strerror(int code);
 int tbg_device_count(void);
+/* Compute units of HIP device `device` (the engine's SIMD count / 4), or a
+ * negative TBG_E_* code.  Lets a host size work for the launch shape without
+ * another HIP runtime in the process (a second libamdhip64 -- e.g. PyTorch's
+ * bundled copy -- that initialises after this library's finds no devices). */
+int tbg_device_cu_count(int device);
+/* Wait for every stream of the context (slots, express slot, utility
+ * stream): the bench's "synchronize" on both sides of its timed region. */
+int tbg_synchronize(tbg_ctx* ctx);
 
 /* Decode and validate `count` 48-byte compressed G1 public keys on the GPU
  * and append them to the resident table.  Ids are first_id .. first_id+count-1.

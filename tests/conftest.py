@@ -23,16 +23,9 @@ def progress(msg: str) -> None:
         f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
     print(msg, file=sys.stderr, flush=True)
 
-
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_first(request):
-    """GPU tests that ask torch for device properties (test_gpu_shape,
-    test_gpu_replay_shape) need torch's HIP runtime initialised before the
-    engine library's own first HIP calls in the process: torch's lazy init
-    reported "No HIP GPUs are available" when it came second.  Initialise it
-    up front whenever a GPU test is selected."""
-    if any(item.get_closest_marker("gpu") for item in request.session.items):
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.init()
-    yield
+# No test asks torch.cuda anything: device facts come from the engine library
+# (tbg_device_count / tbg_device_cu_count).  PyTorch's wheel bundles its own
+# libamdhip64.so, which its libraries NEED by the unversioned name: loaded
+# after the engine library (ROCm's libamdhip64.so.7) it maps as a SECOND HIP
+# runtime, and whichever of the two initialises second finds no devices --
+# the round-5 "No HIP GPUs are available" (DESIGN.md section 5).

@@ -17,7 +17,7 @@ def _free_port():
 
 def _worker(rank, ws, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port), TBG_DIST_BACKEND="gloo")
+                      MASTER_PORT=str(port))
     import time
     import bench
     w, r, _ = bench.dist_setup()
@@ -48,6 +48,40 @@ def test_two_rank_max_over_ranks():
     # both ranks report the same (max) elapsed time, at least the slow rank's 0.2 s
     assert abs(dts[0] - dts[1]) < 1e-9
     assert dts[0] >= 0.2
+
+
+def _bench(args, env_extra=None, timeout=180):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_gpus_n_without_launcher_spawns_n_ranks():
+    """`bench.py --gpus 2` with WORLD_SIZE unset starts two
+    rank processes itself (gloo barrier, max over ranks); rank 0 prints one
+    JSON line naming both ranks, each its own process on LOCAL_RANK = rank."""
+    import json
+    r = _bench(["--gpus", "2", "--steps", "2", "--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, r.stdout  # stdout carries the JSON line alone (gloo's own messages go to stderr)
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    ranks = sorted(tuple(x) for x in out["ranks"])
+    assert [(x[0], x[1]) for x in ranks] == [(0, 0), (1, 1)]
+    assert ranks[0][2] != ranks[1][2]  # two processes
+    assert out["elapsed_max_s"] >= 0.2  # the slower rank's 2 x 0.1 s
+
+
+def test_gpus_must_match_world_size():
+    """Under a launcher --gpus N must equal WORLD_SIZE (a mismatch would time
+    one GPU and call it N)."""
+    r = _bench(["--gpus", "8", "--launch-check"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
 
 
 def test_roofline_fields_from_work_model():

@@ -112,10 +112,9 @@ def test_multi_device_config4_shard(engine):
     """Config 4's 125k-DV shard through tbg_multi_* (3 contexts on the visible
     device(s)): the gathered results equal per-shard single-context runs
     bit-exactly, and oracle/c on a 10k-DV slice."""
-    import torch
     from charon_amd import engine as eng
     from tools.workload import make_mixed_batch
-    ndev = max(1, torch.cuda.device_count())
+    ndev = max(1, eng.device_count())
     m = eng.MultiEngine([i % ndev for i in range(3)], slots=1)
     try:
         b = make_mixed_batch(engine, 125000, seed=404, inject=0.01, thresholds=((3, 4),), load=m.load_pubkeys)

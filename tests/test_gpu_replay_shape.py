@@ -19,11 +19,10 @@ PREFIX = [7, 7, 6]
 
 
 def test_replay_plan_reshaped_launches():
-    import torch
     from charon_amd import engine as eng
     from tests.test_gpu_shape import expected_shape
     from tools.workload import make_batch
-    n_cu = torch.cuda.get_device_properties(0).multi_processor_count  # (before the engine's own HIP calls)
+    n_cu = eng.device_cu_count(0)
     assert expected_shape(DVS * PER_SLOT, n_cu) == (16, 4)
     assert expected_shape(DVS * sum(PREFIX), n_cu) == (14, 7)
     e = eng.Engine(0, slots=SLOTS)
@@ -56,3 +55,46 @@ def test_replay_plan_reshaped_launches():
         assert np.flatnonzero(r.partial_status != eng.PS_VALID).tolist() == [i]
     finally:
         e.close()
+
+
+def test_replay_prefix_keeps_shape_its_chunk_arena_cannot_hold():
+    """a replay may only reshape a launch where EVERY
+    group / chunk section of the slot's arena holds the new shape.  A slot
+    submitted as 90k + 70k duties is sized at (16, 8) (20,000 chunks); its
+    90k-duty prefix alone would take (16, 4) -- 22,500 chunks, more than the
+    chunk lists and chunk values hold -- so the replay must keep (16, 8).
+    With 20 % invalid partials nearly every group fails level 0 and level 1,
+    so the chunk-level kernels write every chunk slot: the prefix must still
+    equal its known answer."""
+    from charon_amd import engine as eng
+    from tests.test_gpu_shape import expected_shape
+    from tools.workload import make_batch
+    n_cu = eng.device_cu_count(0)
+    assert expected_shape(160000, n_cu) == (16, 8)
+    assert expected_shape(90000, n_cu) == (16, 4)
+    e = eng.Engine(0, slots=1, rlc_batch=eng.RLC_L0_ON)
+    try:
+        a = make_batch(e, 90000, 3, 4, seed=9901, inject=0.2)
+        b = make_batch(e, 70000, 3, 4, seed=9902, inject=0.2)
+        ta, tb = e.submit_group(eng.OP_VERIFY_AGGREGATE, [_call(a), _call(b)])
+        _known_answer(e.collect(ta), a)
+        _known_answer(e.collect(tb), b)
+        assert (e.shape(ta)["group"], e.shape(ta)["chunk"]) == (16, 8)
+        assert e.level0(ta) == eng.L0_FAILED
+        e.replay_plan([ta], [1])
+        # the launch ran at the submitted shape, over the prefix's duties
+        sh = e.shape(ta)
+        assert (sh["group"], sh["chunk"]) == (16, 8)
+        assert sh["chunks"] == -(-90000 // 16) * 2
+        _known_answer(e.fetch(ta, a.n_dv, len(a.identifiers)), a)
+    finally:
+        e.close()
+
+
+def test_express_slot_yields_to_the_stream_bound():
+    """slots x streams_per_slot at the stream bound leaves
+    no stream for the express slot; the context runs without one instead of
+    being refused."""
+    from charon_amd import engine as eng
+    e = eng.Engine(0, slots=8, streams_per_slot=2)  # 16 streams: TBG_MAX_SLOT_STREAMS
+    e.close()

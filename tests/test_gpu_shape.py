@@ -47,10 +47,9 @@ def test_shape_mirror():
 
 @pytest.fixture(scope="module")
 def shard():
-    import torch
     from charon_amd import engine as eng
     from tools.workload import make_batch
-    n_cu = torch.cuda.get_device_properties(0).multi_processor_count  # (before the engine's own HIP calls)
+    n_cu = eng.device_cu_count(0)
     e = eng.Engine(0, slots=1)  # group size and chunk not configured: the engine picks them
     b = make_batch(e, DVS, 3, 4, seed=4125)
     yield e, b, n_cu

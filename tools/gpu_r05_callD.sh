@@ -4,7 +4,7 @@
 # and config 4's 125k-DV shard twice, interleaved.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-bash tools/gpu_r04_tests.sh r5t4 || exit 1
+bash tools/gpu_tests.sh r5t4 || exit 1
 O=$R/gpurun_out/r5c8
 mkdir -p $O
 run() {  # name lib out args...

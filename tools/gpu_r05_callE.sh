@@ -5,7 +5,7 @@
 # routings.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-bash tools/gpu_r04_tests.sh r5t5 || exit 1
+bash tools/gpu_tests.sh r5t5 || exit 1
 O=$R/gpurun_out/r5shape
 mkdir -p $O
 run() {  # lib out args...

@@ -6,5 +6,5 @@
 # k_decode_sigs times.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-bash tools/gpu_r04_tests.sh r5t6 || exit 1
+bash tools/gpu_tests.sh r5t6 || exit 1
 C3=1 GATE=0 bash tools/gpu_r05_ab.sh r5sqrt product varlib/dx1.so varlib/c4only.so

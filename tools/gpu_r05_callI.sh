@@ -5,7 +5,7 @@
 # twice, 48 steps, config 4, config 3.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-bash tools/gpu_r04_tests.sh r5t9 "tests/test_gpu_shape.py tests/test_gpu_headline.py tests/test_gpu_parity.py $(ls tests/test_gpu_replay*.py 2>/dev/null)" || exit 1
+bash tools/gpu_tests.sh r5t9 "tests/test_gpu_shape.py tests/test_gpu_headline.py tests/test_gpu_parity.py $(ls tests/test_gpu_replay*.py 2>/dev/null)" || exit 1
 O=$R/gpurun_out/r5rs
 mkdir -p $O
 run() {  # lib name args...

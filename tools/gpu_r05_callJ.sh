@@ -4,7 +4,7 @@
 # config 3, 1 % invalid.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-bash tools/gpu_r04_tests.sh r5t10 || exit 1
+bash tools/gpu_tests.sh r5t10 || exit 1
 O=$R/gpurun_out/r5pk
 mkdir -p $O
 run() {  # lib name args...

@@ -5,7 +5,7 @@
 # config 3.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-bash tools/gpu_r04_tests.sh r5t13 "tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_fullsize.py::test_config2_full_batch_matches_oracle tests/test_gpu_replay_shape.py tests/test_gpu_shape.py" || exit 1
+bash tools/gpu_tests.sh r5t13 "tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_fullsize.py::test_config2_full_batch_matches_oracle tests/test_gpu_replay_shape.py tests/test_gpu_shape.py" || exit 1
 O=$R/gpurun_out/r5rc
 mkdir -p $O
 run() {  # lib name args...

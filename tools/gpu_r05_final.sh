@@ -8,7 +8,7 @@ D=${1:-r5final}
 O=$R/gpurun_out/$D
 mkdir -p $O
 cd $R
-bash tools/gpu_r04_tests.sh $D || exit 1
+bash tools/gpu_tests.sh $D || exit 1
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 cd /tmp && export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # The -m gpu suite (or the tests named in $2) in one process, progress per
 # test in gpurun_out/<dir>/tests.log; bounded; stops at the first failure.
-#   bash tools/gpu_r04_tests.sh <outdir> [pytest selection]
+#   bash tools/gpu_tests.sh <outdir> [pytest selection]
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${1:-r4tests}
 SEL=${2:-tests}
