@@ -74,7 +74,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_subgroup_sigs(DevBatch B) {
   const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (i >= B.n_partials) return;
   if (B.partial_status[i] != TBG_PS_NOT_VERIFIED) return;
-  if (B.sgb && !B.sgb_bad[i / SGB_M]) return;  // every combination of its group is in G2 (k_sgb.hip)
+  if (B.sgb && !B.sgb_bad[i / B.sgb_m]) return;  // every combination of its group is in G2 (k_sgb.hip)
   const Aff<Fp2x> a = px_load(B.sig_aff[i]);
   bool exc = false;
   bool ok = g2_in_subgroup_aff_g(a, exc);

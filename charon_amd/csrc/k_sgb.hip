@@ -35,15 +35,14 @@
 namespace tbg {
 
 constexpr uint32_t kSgbSortBlock = 256;
-constexpr uint32_t SGB_ENT = SGB_M * SGB_K;  // entry capacity per group
 
 __global__ void __launch_bounds__(kSgbSortBlock) k_sgb_sort(DevBatch B) {
   __shared__ uint32_t cnt[SGB_BUCKETS];
   __shared__ uint32_t off[SGB_BUCKETS + 1];
-  __shared__ int8_t dig[SGB_M * SGB_K];
-  const uint32_t g = blockIdx.x, t = threadIdx.x;
-  const uint32_t i0 = g * SGB_M;
-  const uint32_t n = min(SGB_M, B.n_partials - i0);
+  __shared__ int8_t dig[SGB_M * SGB_K];  // (the largest group)
+  const uint32_t g = blockIdx.x, t = threadIdx.x, m = B.sgb_m;
+  const uint32_t i0 = g * m;
+  const uint32_t n = min(m, B.n_partials - i0);
   for (uint32_t b = t; b < SGB_BUCKETS; b += kSgbSortBlock) cnt[b] = 0;
   if (t == 0) B.sgb_bad[g] = 0;
   __syncthreads();
@@ -74,7 +73,7 @@ __global__ void __launch_bounds__(kSgbSortBlock) k_sgb_sort(DevBatch B) {
     if (b < SGB_BUCKETS) cnt[b] = off[b];  // scatter cursors
   }
   __syncthreads();
-  uint32_t* ent = B.sgb_ent + (size_t)SGB_ENT * g;
+  uint32_t* ent = B.sgb_ent + (size_t)m * SGB_K * g;
   for (uint32_t li = t; li < n; li += kSgbSortBlock) {
 #pragma unroll 1
     for (uint32_t k = 0; k < SGB_K; ++k) {
@@ -89,13 +88,14 @@ __global__ void __launch_bounds__(kSgbSortBlock) k_sgb_sort(DevBatch B) {
 // one lane pair per (group, bucket, slice)
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_bucket(DevBatch B, uint32_t n_sg) {
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
-  if (w >= n_sg * SGB_BUCKETS * SGB_SPLIT) return;
-  const uint32_t g = w / (SGB_BUCKETS * SGB_SPLIT), b = (w / SGB_SPLIT) % SGB_BUCKETS, sl = w % SGB_SPLIT;
+  const uint32_t S = B.sgb_split, m = B.sgb_m;
+  if (w >= n_sg * SGB_BUCKETS * S) return;
+  const uint32_t g = w / (SGB_BUCKETS * S), b = (w / S) % SGB_BUCKETS, sl = w % S;
   const uint32_t* goff = B.sgb_off + (size_t)(SGB_BUCKETS + 1) * g;
   const uint32_t o0 = goff[b], n = goff[b + 1] - o0;
-  const uint32_t e0 = o0 + (n * sl) / SGB_SPLIT, e1 = o0 + (n * (sl + 1)) / SGB_SPLIT;
-  const uint32_t* ent = B.sgb_ent + (size_t)SGB_ENT * g;
-  const G2A* sig = B.sig_aff + (size_t)SGB_M * g;
+  const uint32_t e0 = o0 + (n * sl) / S, e1 = o0 + (n * (sl + 1)) / S;
+  const uint32_t* ent = B.sgb_ent + (size_t)m * SGB_K * g;
+  const G2A* sig = B.sig_aff + (size_t)m * g;
   Jac<Fp2x> acc = jac_inf<Fp2x>();
 #pragma unroll 1
   for (uint32_t e = e0; e < e1; ++e) {
@@ -118,11 +118,12 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_bucket(DevBatch B, uint32_t n
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_fold(DevBatch B, uint32_t n_sg) {
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (w >= n_sg * SGB_BUCKETS) return;
-  G2J* part = B.sgb_part + (size_t)w * SGB_SPLIT;
+  const uint32_t S = B.sgb_split;
+  G2J* part = B.sgb_part + (size_t)w * S;
   Jac<Fp2x> acc = px_load(part[0]);
   bool exc = false;
 #pragma unroll 1
-  for (uint32_t sl = 1; sl < SGB_SPLIT; ++sl) acc = jac_add_x(acc, px_load(part[sl]), exc);
+  for (uint32_t sl = 1; sl < S; ++sl) acc = jac_add_x(acc, px_load(part[sl]), exc);
   if (pair_all(!exc)) px_store(part[0], acc);
   else if (pair_par() == 0) B.sgb_bad[w / SGB_BUCKETS] = 1u;
 }
@@ -133,13 +134,13 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_fold(DevBatch B, uint32_t n_s
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_combine(DevBatch B, uint32_t n_sg) {
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (w >= n_sg * SGB_K) return;
-  const uint32_t g = w / SGB_K, k = w % SGB_K;
-  G2J* part = B.sgb_part + ((size_t)SGB_BUCKETS * g + (size_t)SGB_V * k) * SGB_SPLIT;
+  const uint32_t g = w / SGB_K, k = w % SGB_K, S = B.sgb_split;
+  G2J* part = B.sgb_part + ((size_t)SGB_BUCKETS * g + (size_t)SGB_V * k) * S;
   Jac<Fp2x> run = jac_inf<Fp2x>(), q = run;
   bool exc = false;
 #pragma unroll 1
   for (int v = (int)SGB_V; v >= 1; --v) {
-    run = jac_add_x(run, px_load(part[(size_t)(v - 1) * SGB_SPLIT]), exc);
+    run = jac_add_x(run, px_load(part[(size_t)(v - 1) * S]), exc);
     q = jac_add_x(q, run, exc);
   }
   if (pair_all(!exc)) px_store(part[0], q);
@@ -153,7 +154,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_test(DevBatch B, uint32_t n_s
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (w >= n_sg * SGB_K) return;
   const uint32_t g = w / SGB_K, k = w % SGB_K;
-  const Jac<Fp2x> q = px_load(B.sgb_part[((size_t)SGB_BUCKETS * g + (size_t)SGB_V * k) * SGB_SPLIT]);
+  const Jac<Fp2x> q = px_load(B.sgb_part[((size_t)SGB_BUCKETS * g + (size_t)SGB_V * k) * B.sgb_split]);
   bool ok = true;
   if (!jac_is_inf(q)) {
     bool exc = false;
@@ -171,11 +172,12 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_test(DevBatch B, uint32_t n_s
 }
 
 void launch_subgroup_batch(const DevBatch& B, hipStream_t st) {
-  const uint32_t n_sg = sgb_groups(B.n_partials);
-  if (!B.sgb || !n_sg) return;
+  if (!B.sgb) return;
+  const uint32_t n_sg = sgb_groups(B.n_partials, B.sgb_m);
+  if (!n_sg) return;
   TBG_KLAUNCH(k_sgb_sort, dim3(n_sg), dim3(kSgbSortBlock), st, B);
-  TBG_KLAUNCH(k_sgb_bucket, grid_for(2 * n_sg * SGB_BUCKETS * SGB_SPLIT), dim3(kBlock), st, B, n_sg);
-  if (SGB_SPLIT > 1) TBG_KLAUNCH(k_sgb_fold, grid_for(2 * n_sg * SGB_BUCKETS), dim3(kBlock), st, B, n_sg);
+  TBG_KLAUNCH(k_sgb_bucket, grid_for(2 * n_sg * SGB_BUCKETS * B.sgb_split), dim3(kBlock), st, B, n_sg);
+  if (B.sgb_split > 1) TBG_KLAUNCH(k_sgb_fold, grid_for(2 * n_sg * SGB_BUCKETS), dim3(kBlock), st, B, n_sg);
   TBG_KLAUNCH(k_sgb_combine, grid_for(2 * n_sg * SGB_K), dim3(kBlock), st, B, n_sg);
   TBG_KLAUNCH(k_sgb_test, grid_for(2 * n_sg * SGB_K), dim3(kBlock), st, B, n_sg);
 }

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cmath>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -612,6 +613,30 @@ static bool l0_shape_fits(uint32_t nd0, uint32_t G0, uint32_t C0, uint32_t nd, u
          (G <= 64) == (G0 <= 64);
 }
 
+// Batched subgroup test plan from the non-subgroup share `rho` of the
+// collected partials.  Per signature, in units of one
+// per-signature test (psi(s) == [x] s: 63 doublings + 5 additions): the 16.6
+// bucket additions with the sort and running sums 0.55 (measured: k_sgb_*
+// 0.47-0.57 of k_subgroup_sigs' time per signature, profiles/r06/sgb), the
+// group's 18 tests 1.1 x 18 / m (each on a lone lane pair), and the failed
+// groups' members tested alone 1 - (1 - rho)^m.  The group size m is the
+// cheapest power of two in [SGB_M_MIN, SGB_M]; the test runs while that
+// costs under 0.95 of testing every signature alone -- up to rho ~ 2.5e-3
+// (TBG_SGB_AUTO_MAX).  Clean traffic keeps m = 1,024; config 5's 1.25e-3
+// takes m = 128 (at 1,024, 72 % of its groups would fail).
+static bool sgb_plan(double rho, uint32_t& m) {
+  double best = 1e9;
+  m = SGB_M;
+  for (uint32_t k = SGB_M; k >= SGB_M_MIN; k >>= 1) {
+    const double cost = 0.55 + 1.1 * (double)SGB_K / k + (1.0 - std::pow(1.0 - std::min(rho, 1.0), (double)k));
+    if (cost < best - 1e-12) {
+      best = cost;
+      m = k;
+    }
+  }
+  return best < 0.95;
+}
+
 int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches, tbg_ticket* tickets) {
   if (!c || !bs || !tickets || n_batches == 0) return TBG_E_INVALID_ARG;
   int rc;
@@ -725,12 +750,14 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   // Batched subgroup test while the collected batches carry (almost) no
   // non-subgroup signature: groups of 1,024 partials, a failed group's members
   // tested alone (k_sgb.hip); small batches test every signature alone.
-  const bool sgb = np >= SGB_MIN_PARTIALS &&
-                   (c->sgb_mode == TBG_SGB_ON || (c->sgb_mode == TBG_SGB_AUTO && c->nonsub_ema < TBG_SGB_AUTO_MAX));
-  const size_t n_sg = sgb ? sgb_groups(np) : 0;
+  uint32_t sgb_m = SGB_M;
+  const bool sgb = np >= SGB_MIN_PARTIALS && c->sgb_mode != TBG_SGB_OFF &&
+                   (sgb_plan(c->nonsub_ema, sgb_m) || c->sgb_mode == TBG_SGB_ON);
+  const uint32_t sgb_split = sgb_split_for(sgb_m);
+  const size_t n_sg = sgb ? sgb_groups(np, sgb_m) : 0;
   size_t w_sgoff = sec(4ull * (SGB_BUCKETS + 1) * n_sg);
-  size_t w_sgent = sec(4ull * SGB_M * SGB_K * n_sg);
-  size_t w_sgpart = sec(sizeof(G2J) * SGB_BUCKETS * SGB_SPLIT * n_sg);
+  size_t w_sgent = sec(4ull * sgb_m * SGB_K * n_sg);
+  size_t w_sgpart = sec(sizeof(G2J) * SGB_BUCKETS * sgb_split * n_sg);
   size_t w_sgbad = sec(4ull * n_sg);
   size_t w_aacc = sec(op != TBG_OP_VERIFY ? sizeof(G2J) * (size_t)nd : 0);
   size_t w_alist = sec(op != TBG_OP_VERIFY ? 4ull * nd : 0);
@@ -925,6 +952,8 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.batch_f = (uint32_t*)(dw + w_bf);
   B.grp_f = (uint32_t*)(dw + w_gf);
   B.sgb = sgb ? 1u : 0u;
+  B.sgb_m = sgb_m;
+  B.sgb_split = sgb_split;
   B.sgb_off = (uint32_t*)(dw + w_sgoff);
   B.sgb_ent = (uint32_t*)(dw + w_sgent);
   B.sgb_part = (G2J*)(dw + w_sgpart);
@@ -1271,20 +1300,21 @@ int tbg_fetch_shape(tbg_ctx* c, tbg_ticket t, uint32_t* out4) {
   return TBG_OK;
 }
 
-int tbg_fetch_subgroup(tbg_ctx* c, tbg_ticket t, uint32_t* out2) {
-  if (!c || !out2) return TBG_E_INVALID_ARG;
+int tbg_fetch_subgroup(tbg_ctx* c, tbg_ticket t, uint32_t* out3) {
+  if (!c || !out3) return TBG_E_INVALID_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   Slot* s = find_ticket(c, t, false, nullptr);
   if (!s) return TBG_E_TICKET;
   HIP_TRY(hipSetDevice(c->device));
-  out2[0] = out2[1] = 0;
+  out3[0] = out3[1] = out3[2] = 0;
   if (!s->last.sgb) return TBG_OK;
-  const uint32_t n_sg = sgb_groups(s->last.n_partials);
+  out3[2] = s->last.sgb_m;
+  const uint32_t n_sg = sgb_groups(s->last.n_partials, s->last.sgb_m);
   std::vector<uint32_t> bad(n_sg);
   HIP_TRY(hipMemcpyAsync(bad.data(), s->last.sgb_bad, 4ull * n_sg, hipMemcpyDeviceToHost, s->st));
   HIP_TRY(hipStreamSynchronize(s->st));
-  out2[0] = n_sg;
-  for (uint32_t g = 0; g < n_sg; ++g) out2[1] += bad[g] ? 1u : 0u;
+  out3[0] = n_sg;
+  for (uint32_t g = 0; g < n_sg; ++g) out3[1] += bad[g] ? 1u : 0u;
   return TBG_OK;
 }
 

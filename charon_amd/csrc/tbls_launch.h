@@ -153,12 +153,14 @@ struct DevBatch {
   // c_i uniform mod 13 are tested psi(Q) == [x] Q; only the members of a
   // failed group take the per-signature test (k_subgroup_sigs)
   uint32_t sgb;           // 1: the batched test runs (0: every signature is tested alone)
+  uint32_t sgb_m;         // consecutive partials per group (a power of two, SGB_M_MIN..SGB_M)
+  uint32_t sgb_split;     // slices per bucket (k_sgb_bucket / k_sgb_fold)
   uint32_t sgb_seed[8];   // secret per-batch key of the combinations' digits: always fresh OS
                           // entropy, even under a fixed rlc_seed (a predictable key would let a
                           // submitter craft torsion components that cancel across combinations)
   uint32_t* sgb_off;      // [n_sg][SGB_BUCKETS + 1] bucket offsets into the group's entries
-  uint32_t* sgb_ent;      // [n_sg][SGB_M * SGB_K] entries: member << 1 | negative
-  G2J* sgb_part;          // [n_sg][SGB_BUCKETS][SGB_SPLIT] bucket slice sums
+  uint32_t* sgb_ent;      // [n_sg][sgb_m * SGB_K] entries: member << 1 | negative
+  G2J* sgb_part;          // [n_sg][SGB_BUCKETS][sgb_split] bucket slice sums
   uint32_t* sgb_bad;      // [n_sg] 1: some combination is outside G2 (members tested alone)
   // recombination (k_aggregate.hip)
   G2J* agg_acc;           // [n_duties] integer-coefficient sums awaiting [1/D] (listed duties only)
@@ -194,20 +196,30 @@ constexpr uint32_t MSM_SUM_ENTRIES = 128;
 #ifndef TBG_SGB_SPLIT
 #define TBG_SGB_SPLIT 4
 #endif
-constexpr uint32_t SGB_M = TBG_SGB_M;  // consecutive partials per group
+// The group size follows the non-subgroup share of the collected batches
+// (sgb_plan, tbls_engine.hip): SGB_M while clean, down to SGB_M_MIN when a
+// few signatures per thousand are outside G2 (a failed group costs its
+// members' per-signature tests).
+constexpr uint32_t SGB_M = TBG_SGB_M;  // largest group: consecutive partials (LDS of k_sgb_sort)
+constexpr uint32_t SGB_M_MIN = 64;
 constexpr uint32_t SGB_K = 18;         // combinations per group
 constexpr uint32_t SGB_V = 6;          // buckets per combination (|c| = 1..6)
 constexpr uint32_t SGB_BUCKETS = SGB_K * SGB_V;
-constexpr uint32_t SGB_SPLIT = TBG_SGB_SPLIT;  // slices per bucket (~40 additions each at SGB_M = 1024)
+constexpr uint32_t SGB_SPLIT = TBG_SGB_SPLIT;  // slices per bucket at SGB_M (~40 additions each)
 constexpr uint32_t SGB_MIN_PARTIALS = 2 * SGB_M;  // smaller batches test each signature alone
-TBG_HD inline uint32_t sgb_groups(uint32_t n_partials) { return (n_partials + SGB_M - 1) / SGB_M; }
+TBG_HD uint32_t sgb_groups(uint32_t n_partials, uint32_t m) { return (n_partials + m - 1) / m; }
+// slices per bucket for groups of m: ~40 entries per slice, at least one
+TBG_HD uint32_t sgb_split_for(uint32_t m) {
+  const uint32_t s = SGB_SPLIT * m / SGB_M;
+  return s ? s : 1u;
+}
 // Level-0 product tree over the groups' P-chunk products.  Each pass is a
 // chain of F - 1 Fp12 products on one lane group (~24 us each at one wave per
 // SIMD), so the tree's latency ~ log_F(n) * F is smallest near F = 4 (16: 1.3
 // ms for 10k groups; 4: ~0.7 ms) -- it sits on every launch's critical path.
 constexpr uint32_t L0_TREE_FAN = 4;
 // (sum over the passes of ceil(n / F^k) <= n / (F - 1) + one per pass)
-TBG_HD inline uint32_t grp_f_entries(uint32_t n_groups) { return n_groups + n_groups / (L0_TREE_FAN - 1) + 40; }
+TBG_HD uint32_t grp_f_entries(uint32_t n_groups) { return n_groups + n_groups / (L0_TREE_FAN - 1) + 40; }
 // k_miller_hex modes
 enum MillerMode : int { MILLER_GROUPS = 0, MILLER_L0 = 1, MILLER_GROUP_S = 2 };
 // k_rlc_duty_sum phases

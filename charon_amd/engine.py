@@ -268,11 +268,11 @@ class Engine:
 
     def subgroup(self, ticket) -> dict:
         """Batched subgroup test of the batch's last run (tbg_fetch_subgroup):
-        groups of 1,024 partials tested by random combinations (0: every
-        signature tested alone) and how many failed."""
-        out = np.zeros(2, dtype=np.uint32)
+        groups of consecutive partials tested by random combinations (0:
+        every signature tested alone), how many failed, partials per group."""
+        out = np.zeros(3, dtype=np.uint32)
         self._check(self._lib.tbg_fetch_subgroup(self._h, ticket, _ptr(out)), "tbg_fetch_subgroup")
-        return dict(zip(["groups", "failed"], out.tolist()))
+        return dict(zip(["groups", "failed", "group_size"], out.tolist()))
 
     def host_stats(self, reset=False) -> dict:
         """Host-side work of this context's submit / collect calls (tbg_host_stats)."""

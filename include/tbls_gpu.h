@@ -111,9 +111,11 @@ typedef struct {
                            * longer lists run in several passes                       */
   uint32_t subgroup_batch; /* G2 subgroup checks of the decoded signatures:
                            * TBG_SGB_AUTO (0) random-combination tests per group of
-                           * 1,024 partials, each member tested alone only when its
-                           * group fails, while the non-subgroup share average is
-                           * below TBG_SGB_AUTO_MAX; TBG_SGB_ON always; TBG_SGB_OFF
+                           * consecutive partials, each member tested alone only when
+                           * its group fails; the group size (1,024 down to 64)
+                           * follows the collected batches' non-subgroup share, and
+                           * past ~TBG_SGB_AUTO_MAX every signature is tested alone;
+                           * TBG_SGB_ON always (the same group sizes); TBG_SGB_OFF
                            * every signature alone.  Batches below 2,048 partials
                            * always test each signature alone.                        */
   uint32_t express_partials; /* batches of at most this many partials go to an extra
@@ -127,9 +129,10 @@ typedef struct {
 #define TBG_SGB_AUTO 0
 #define TBG_SGB_ON 1
 #define TBG_SGB_OFF 2
-/* (with 1,024 partials per group ~18 % of the groups fail at this share: the
- * batched test then costs ~0.7 of testing every signature alone) */
-#define TBG_SGB_AUTO_MAX 2e-4
+/* Where the automatic mode stops: past this non-subgroup share even the best
+ * group size (128) fails ~30 % of its groups, and the batched test would cost
+ * more than ~0.95 of testing every signature alone (tbls_engine.hip sgb_plan). */
+#define TBG_SGB_AUTO_MAX 2.5e-3
 #define TBG_GIDENT_OFF 0
 #define TBG_GIDENT_L3 1
 #define TBG_GIDENT_CHUNKS 2
@@ -269,10 +272,10 @@ int tbg_fetch_level0(tbg_ctx* ctx, tbg_ticket ticket, int32_t* state);
  * duties per group, level 0 (TBG_L0_*)]. */
 int tbg_fetch_fallback(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out8);
 /* Batched subgroup test of a collected batch's last run (tbg_config.
- * subgroup_batch): out2 = [groups of 1,024 partials tested by random
+ * subgroup_batch): out3 = [groups of consecutive partials tested by random
  * combinations (0: every signature was tested alone), groups that failed
- * (their members were then tested one by one)]. */
-int tbg_fetch_subgroup(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out2);
+ * (their members were then tested one by one), partials per group]. */
+int tbg_fetch_subgroup(tbg_ctx* ctx, tbg_ticket ticket, uint32_t* out3);
 /* Verification shape of a collected batch's last submit: out4 = [duties per
  * group G, duties per Miller chunk C, level 0 on (1) or off, Miller P-chunk
  * hexads G x C cut the batch into].  A level-0 launch with neither G nor C
