@@ -207,7 +207,9 @@ STAGE_KERNELS = {
     "hash": ["k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
     "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_bucket_part", "k_msm_tree", "k_msm_tree_final", "k_msm_scan", "k_msm_scatter",
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
-                "k_l0_lines", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>"],
+                "k_l0_lines", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>",
+                "k_rlc_g1", "k_rlc_duty_sum<DSUM_P>", "k_gm_sort", "k_gm_bucket", "k_gm_window", "k_gm_combine",
+                "k_gm_failed_list", "k_rlc_partial2_list"],
     "h_lines": ["k_lines_h"],
     "verify": ["k_miller_hex<MILLER_L0>", "k_miller_hex<MILLER_GROUPS>", "k_miller_hex<MILLER_GROUP_S>", "k_l0_fold", "k_l0_tree", "k_l0_final", "k_l0_inv", "k_l0_fe", "k_l0_after",
                "k_rlc_group_final", "k_rlc_resolve_groups", "k_rlc_gident_lines", "k_lines_fold<FOLD_GID>",

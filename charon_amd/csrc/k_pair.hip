@@ -106,6 +106,57 @@ __global__ void __launch_bounds__(BINV_BLOCK, TBG_PAIR_WAVES) k_rlc_partial2(Dev
   }
 }
 
+// List mode (k_gmsm.hip): r_i s_i for the candidates of failed groups only
+// (gm_list, CNT_LAZY entries), after the group checks; the G1 products and
+// the key marks are made, the group's lead is gm_lead.  Lane L owns list
+// entry base + L (its slope denominator in the workgroup's batched
+// inversion), the lane pair runs the G2 products of its two entries, as
+// k_rlc_partial2 does (one entry per pair measured 4.7 vs 4.2 ms at 1 %
+// invalid: the inversion amortised over half the partials).  Grid-stride
+// over the list with a workgroup-uniform trip count.
+__global__ void __launch_bounds__(BINV_BLOCK, TBG_PAIR_WAVES) k_rlc_partial2_list(DevBatch B) {
+  if (B.counters[CNT_L0_OK]) return;
+  const uint32_t nl = B.counters[CNT_LAZY];
+#pragma unroll 1
+  for (uint32_t base = blockIdx.x * blockDim.x; base < nl; base += gridDim.x * blockDim.x) {
+    const uint32_t t = base + threadIdx.x;
+    const bool active = t < nl;
+    const uint32_t i = active ? B.gm_list[t] : 0u;
+    const bool lead = active && B.gm_lead[B.partial_duty[i] / B.rlc_group] == i;
+    const bool work = active && !lead;
+    uint32_t a[4] = {0, 0, 0, 0};
+    Fp2 dx2 = fp2_one();
+    if (lead) {
+      B.part_s[i] = jac_from_aff(B.sig_aff[i]);
+    } else if (work) {
+      rlc_digits(rlc_scalar(B.rlc_seed, i), a);
+      const G2A s = B.sig_aff[i];
+      dx2 = fp2_reduce(fp2_sub(fp2_mul(fp2_conj(s.x), fp2_from_const(PSI_X)), s.x));  // psi(s).x - s.x
+    }
+    const Fp2 inv2 = block_batch_inv2<BINV_WAVES>(dx2, work);  // every thread of the workgroup
+    for (uint32_t j = 0; j < 2; ++j) {
+      if (!u32_from_owner(work ? 1u : 0u, j)) continue;  // pair-uniform
+      const uint32_t owner = u32_from_owner(i, j);  // the listed partial of the pair's lane j
+      const Fp2x ix = px_from_owner(inv2, j);
+      uint32_t u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = u32_from_owner(a[k], j);
+      const Aff<Fp2x> s = px_load(B.sig_aff[owner]);
+      const Aff<Fp2x> ps{f_mulc(f_conj(s.x), PSI_X), f_mulc(f_conj(s.y), PSI_Y)};  // psi(s) = [x] s
+      Aff<Fp2x> ap, am;
+      rlc_pair_from_inv(s, ps, ix, ap, am);
+      px_store(B.part_s[owner], rlc_mul_table(ap, am, fp_from_const(PSI2_X), u));
+    }
+  }
+}
+
+void launch_rlc_partials_list(const DevBatch& B, const G1A* pk_aff, hipStream_t st) {
+  (void)pk_aff;
+  uint32_t blocks = (B.n_partials + BINV_BLOCK - 1) / BINV_BLOCK;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks) TBG_KLAUNCH(k_rlc_partial2_list, dim3(blocks), dim3(BINV_BLOCK), st, B);
+}
+
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st) {
   if (!B.n_partials) return;

@@ -82,6 +82,11 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_rlc_duty_sum(DevBatch B) {
   const bool in = d < B.n_duties;
   if (phase == DSUM_FALLBACK_S) {  // (no inversion: no workgroup-wide step)
     if (!in || B.counters[CNT_L0_OK] || B.dv_state[d] != RLC_COMBINED) return;
+#if TBG_GMSM
+    // after the group checks: the failed groups' duties (their r_i s_i were formed)
+    const int32_t gs = B.grp_state[d / B.rlc_group];
+    if (gs != GRP_FAIL && gs != GRP_GID) return;
+#endif
     G2J S = jac_inf<Fp2>();
     for (uint32_t i = B.duty_first[d]; i < B.duty_first[d + 1]; ++i)
       if (rlc_candidate(B, i)) S = jac_add(S, B.part_s[i]);
@@ -109,7 +114,7 @@ __global__ void __launch_bounds__(BINV_BLOCK) k_rlc_duty_sum(DevBatch B) {
   }
   if (!aff || (phase == DSUM_BOTH && jac_is_inf(S))) {
     B.dv_state[d] = RLC_EACH;  // degenerate combination: check the partials one by one
-    if (phase == DSUM_L0_P) B.counters[CNT_L0_BAD] = 1;
+    if (phase == DSUM_L0_P) B.counters[CNT_L0_BAD] = 1;  // (DSUM_P: the group levels only)
     return;
   }
   B.dv_p[d] = G1A{fp_reduce(fp_neg(Pa.x)), Pa.y};  // (-x, y): the Miller steps' evaluation operands
@@ -889,9 +894,16 @@ void launch_rlc_prepare(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff
     return;
   }
   if (after_keys) after_keys(B, st);
+#if TBG_GMSM
+  // the G1 products and P_d, then each group's S by its bucket MSM
+  launch_rlc_g1(B, pk_tab, pk_aff, pk_status, n_pk, st);
+  TBG_KLAUNCH(k_rlc_duty_sum<DSUM_P>, duty_grid(B), dim3(BINV_BLOCK), st, B);
+  launch_gm_group_s(B, st);
+#else
   launch_rlc_partials(B, pk_tab, pk_aff, pk_status, n_pk, st);
   TBG_KLAUNCH(k_rlc_duty_sum<DSUM_BOTH>, duty_grid(B), dim3(BINV_BLOCK), st, B);
   TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
+#endif
   launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
 }
 
@@ -919,9 +931,13 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
       TBG_KLAUNCH(k_l0_after, grid_for(n_groups), dim3(kBlock), st, B);
       // level 0 failed: the group levels' signature side (these kernels
       // return at once after a pass)
+#if TBG_GMSM
+      launch_gm_group_s(B, st);  // (G1 products, P_d and r_i: level 0's)
+#else
       launch_rlc_partials(B, nullptr, pk_aff, pk_status, n_pk, st);  // (G1 products: level 0's)
       TBG_KLAUNCH(k_rlc_duty_sum<DSUM_FALLBACK_S>, duty_grid(B), dim3(BINV_BLOCK), st, B);
       TBG_KLAUNCH(k_rlc_group_lines, grid_for(n_groups), dim3(kBlock), st, B);
+#endif
       launch_lines_fold(B, FOLD_GROUPS, n_groups, st);
       launch_group_s_miller_hex(B, st);
     } else {
@@ -929,6 +945,11 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
     }
     TBG_KLAUNCH(k_rlc_group_final, grid_for(hex_threads(n_groups)), dim3(kBlock), st, B);
     TBG_KLAUNCH(k_rlc_resolve_groups, grid_for(B.n_duties), dim3(kBlock), st, B);
+#if TBG_GMSM
+    // the failed groups' r_i s_i and S_d, which every deeper level reads
+    launch_gm_failed_partials(B, pk_aff, st);
+    TBG_KLAUNCH(k_rlc_duty_sum<DSUM_FALLBACK_S>, duty_grid(B), dim3(BINV_BLOCK), st, B);
+#endif
     if (B.rlc_group > 1) {
       // level 1g before the chunks: its unresolved groups add to the chunk list
       uint32_t W = 1;

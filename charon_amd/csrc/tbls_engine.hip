@@ -747,6 +747,15 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   size_t w_blines = sec(l0 ? 4ull * LINES_WORDS : 0);
   size_t w_bf = sec(l0 ? 4ull * 3 * 4 * NL : 0);
   size_t w_gf = sec(l0 ? 4ull * 3 * 4 * NL * grp_f_entries(ng) : 0);
+  // level 1's group MSM (k_gmsm.hip): entries, offsets, bucket sums, leads, the failed groups' candidates
+  const bool gm = TBG_GMSM && G != 0;
+  size_t w_gmoff = sec(gm ? 4ull * (GM_BUCKETS + 1) * ng : 0);
+  size_t w_gment = sec(gm ? 64ull * np : 0);
+  size_t w_gmpart = sec(gm ? sizeof(G2J) * GM_BUCKETS * (size_t)ng : 0);
+  size_t w_gmlead = sec(gm ? 4ull * ng : 0);
+  size_t w_gmlist = sec(gm ? 4ull * np : 0);
+  size_t w_gmhist = sec(gm ? 4ull * 256 : 0);
+  size_t w_gmorder = sec(gm ? 4ull * GM_BUCKETS * ng : 0);
   // Batched subgroup test while the collected batches carry (almost) no
   // non-subgroup signature: groups of 1,024 partials, a failed group's members
   // tested alone (k_sgb.hip); small batches test every signature alone.
@@ -951,6 +960,13 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.batch_lines = (uint32_t*)(dw + w_blines);
   B.batch_f = (uint32_t*)(dw + w_bf);
   B.grp_f = (uint32_t*)(dw + w_gf);
+  B.gm_off = (uint32_t*)(dw + w_gmoff);
+  B.gm_ent = (uint32_t*)(dw + w_gment);
+  B.gm_part = (G2J*)(dw + w_gmpart);
+  B.gm_lead = (uint32_t*)(dw + w_gmlead);
+  B.gm_list = (uint32_t*)(dw + w_gmlist);
+  B.gm_hist = (uint32_t*)(dw + w_gmhist);
+  B.gm_order = (uint32_t*)(dw + w_gmorder);
   B.sgb = sgb ? 1u : 0u;
   B.sgb_m = sgb_m;
   B.sgb_split = sgb_split;

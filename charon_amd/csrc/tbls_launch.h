@@ -148,6 +148,18 @@ struct DevBatch {
   uint32_t* batch_lines;  // [LINES_WORDS] Miller lines of S (-g1 folded in)
   uint32_t* batch_f;      // [3][4 NL] Miller product of the S pair (quad layout)
   uint32_t* grp_f;        // [GRP_F_ENTRIES(n_groups)][3][4 NL] each group's P-chunk product, then the product tree
+  // level 1's group sums S_g = sum_i r_i s_i as one bucket MSM per group
+  // (k_gmsm.hip): 4-bit windows of the four psi digits,
+  // no per-partial G2 scalar multiplication; the per-partial products r_i s_i
+  // are formed afterwards for the failed groups' candidates only
+  uint32_t* gm_off;       // [n_groups][GM_BUCKETS + 1] bucket offsets into the group's entries
+  uint32_t* gm_ent;       // [16 n_partials] entries (partial << 3 | k << 1 | negative); group g's
+                          // start at 16 * (its first partial)
+  G2J* gm_part;           // [n_groups][GM_BUCKETS] bucket sums, then the window sums T_w at w * GM_V
+  uint32_t* gm_lead;      // [n_groups] the group's r = 1 partial (UINT32_MAX: none / level 0's scalars)
+  uint32_t* gm_list;      // [n_partials] candidates of failed groups, whose r_i s_i are formed afterwards
+  uint32_t* gm_hist;      // [256] bucket-size histogram, then the size-order cursors
+  uint32_t* gm_order;     // [n_groups * GM_BUCKETS] buckets by decreasing size (k_gm_bucket's order)
   // batched subgroup test of the decoded signatures (k_sgb.hip): per group
   // of SGB_M consecutive partials, SGB_K random combinations sum c_i s_i with
   // c_i uniform mod 13 are tested psi(Q) == [x] Q; only the members of a
@@ -177,7 +189,8 @@ enum GroupState : int32_t { GRP_EMPTY = 0, GRP_LINES = 1, GRP_OK = 2, GRP_FAIL =
 // CNT_CHUNKS: level-1.5 chunks, CNT_CID: level-1.5b chunks, CNT_L0_BAD: level 0 cannot
 // hold (a degenerate sum, a duty checked per partial, an unusable H(m)), CNT_L0_OK: level 0 passed
 enum Counter : int { CNT_DUTIES = 0, CNT_PARTIALS = 1, CNT_AGG = 2, CNT_CHUNKS = 3, CNT_CID = 4, CNT_L0_BAD = 5,
-                     CNT_L0_OK = 6, CNT_GID = 7, CNT_WORDS = 8 };  // CNT_GID: level-1g groups
+                     CNT_L0_OK = 6, CNT_GID = 7, CNT_LAZY = 8, CNT_WORDS = 9 };  // CNT_GID: level-1g groups,
+                                                                                // CNT_LAZY: gm_list entries
 
 // Level-0 MSM: a digit a (odd, |a| < 2^16) of r_i puts psi^k(s_i) into bucket
 // (|a| - 1) / 2; the tree sums (k_msm_tree) leave one point per workgroup in
@@ -223,7 +236,18 @@ TBG_HD uint32_t grp_f_entries(uint32_t n_groups) { return n_groups + n_groups / 
 // k_miller_hex modes
 enum MillerMode : int { MILLER_GROUPS = 0, MILLER_L0 = 1, MILLER_GROUP_S = 2 };
 // k_rlc_duty_sum phases
-enum DutySumPhase : int { DSUM_BOTH = 0, DSUM_L0_P = 1, DSUM_FALLBACK_S = 2 };
+//   DSUM_P: P_d only (level 1's S comes from the group MSM, k_gmsm.hip);
+//   DSUM_FALLBACK_S: S_d of the failed groups' duties, from the r_i s_i formed
+//   for them after the group checks
+enum DutySumPhase : int { DSUM_BOTH = 0, DSUM_L0_P = 1, DSUM_FALLBACK_S = 2, DSUM_P = 3 };
+// Level 1's group MSM (k_gmsm.hip): each 16-bit digit a_k of r_i (bls_rlc.h)
+// read as four 4-bit windows of signed binary digits, v = 2 nibble - 15 (odd,
+// |v| <= 15): 16 entries per partial into GM_BUCKETS = 4 windows x 8 buckets
+// (|v| = 2b + 1) per group.
+#ifndef TBG_GMSM
+#define TBG_GMSM 1  // 0: the per-partial products r_i s_i for every candidate (k_rlc_partial2, before round 6)
+#endif
+constexpr uint32_t GM_W = 4, GM_V = 8, GM_BUCKETS = GM_W * GM_V;
 
 // Flags in the fallback lists (k_rlc.hip): the entry's sum is the point at
 // infinity -- no lines, its members go to an exact level.
@@ -318,6 +342,15 @@ void launch_group_s_miller_hex(const DevBatch& B, hipStream_t st);
 // pk_tab: the keys' pair tables (k_pubkey_tables); unused after a level-0 failure (level 0 formed the G1 products)
 void launch_rlc_partials(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status,
                          uint32_t n_pk, hipStream_t st);
+// level 1 by group MSMs (k_gmsm.hip): the G1 products and key marks (no
+// level 0), the groups' S in affine form in pend_pts (grp_state set as
+// k_rlc_group_lines does), and after the group checks the failed groups'
+// r_i s_i (k_pair.hip, list mode) and S_d
+void launch_rlc_g1(const DevBatch& B, const G1A* pk_tab, const G1A* pk_aff, const int32_t* pk_status, uint32_t n_pk,
+                   hipStream_t st);
+void launch_gm_group_s(const DevBatch& B, hipStream_t st);
+void launch_gm_failed_partials(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
+void launch_rlc_partials_list(const DevBatch& B, const G1A* pk_aff, hipStream_t st);
 // spec: the speculative pass (level 0 on, before verification; skipped when
 // level 0 already cannot pass); the regular pass then returns at once if
 // level 0 passed (TBG_SPEC_ALWAYS: see above)

@@ -783,6 +783,25 @@ int hc_msm_check(const uint8_t* sigs96, const uint64_t* r, uint32_t n) {
   G2J got = msm_reference(s, r, n, buckets);
   return jac_eq(got, ref) ? 1 : 0;
 }
+
+// Level 1's group MSM (k_gmsm.hip, 4-bit windows of the psi digits) against
+// the per-partial RLC products; partial `lead` takes r = 1.
+int hc_gm_check(const uint8_t* sigs96, const uint64_t* r, uint32_t n, uint32_t lead) {
+  G2A s[64];
+  if (n > 64) return -2;
+  G2J ref = jac_inf<Fp2>();
+  for (uint32_t i = 0; i < n; ++i) {
+    if (g2_decompress(sigs96 + 96ull * i, s[i]) != DEC_OK) return -1;
+    if (i == lead) {
+      ref = jac_add(ref, jac_from_aff(s[i]));
+      continue;
+    }
+    uint32_t a[4];
+    rlc_digits(r[i], a);
+    ref = jac_add(ref, rlc_mul_g2(s[i], a));
+  }
+  return jac_eq(gm_reference(s, r, n, lead), ref) ? 1 : 0;
+}
 }  // extern "C"
 
 // Level-0 stages (tools/count_work.py): one partial's G1 product from the

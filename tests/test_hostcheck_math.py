@@ -420,6 +420,33 @@ def test_level0_bucket_msm_matches_rlc_products():
         assert L.hc_msm_check(buf, arr, len(ss)) == 1
 
 
+def test_group_msm_windows_match_per_partial_products():
+    """Level 1's group MSM (k_gmsm.hip: each 16-bit psi digit as four 4-bit
+    windows of signed binary digits, 32 buckets, running sums, base-16
+    combination; bls_msm.h gm_reference) equals the sum of the per-partial RLC
+    products rlc_mul_g2 it replaces -- with a group lead (r = 1), a point
+    added twice with the same digits (bucket doublings), s and -s cancelling,
+    and the extreme digit words."""
+    import ctypes
+    L = lib()
+    L.hc_gm_check.restype = ctypes.c_int
+    L.hc_gm_check.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    sigs = [bls.g2_compress(tb.sign(rng.randrange(1, bls.R), bytes([k + 40]) * 32)) for k in range(6)]
+    neg = bls.g2_compress(bls.g2_neg(bls.g2_decompress(sigs[1])))
+    rs = [rng.getrandbits(64) for _ in range(6)]
+    cases = [
+        (sigs, rs, 99),
+        (sigs, rs, 0),                                       # the first partial as the group lead
+        (sigs[:2] + [sigs[0]], rs[:2] + [rs[0]], 99),        # same point, same digits: doublings in 16 buckets
+        ([sigs[1], neg, sigs[2]], [rs[1], rs[1], rs[2]], 99),  # s and -s with the same digits cancel
+        (sigs[:3], [0, 0xFFFF_FFFF_FFFF_FFFF, 0x8000_7FFF_0000_FFFF], 1),
+    ]
+    for ss, rr, lead in cases:
+        buf = b"".join(ss)
+        arr = (ctypes.c_uint64 * len(rr))(*rr)
+        assert L.hc_gm_check(buf, arr, len(ss), lead) == 1, lead
+
+
 def test_word_sha_expand_message_matches_byte_stream():
     """The kernels' expand_message_xmd (16-word blocks in registers, unrolled
     SHA-256 schedule) equals the byte-stream form on every message length
