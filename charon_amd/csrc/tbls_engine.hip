@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <cmath>
+#include <functional>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -583,20 +584,42 @@ static double l0_shape_cost(uint64_t nd, uint32_t n_simd, uint32_t g, uint32_t c
   const uint64_t waves = (hexads + 9) / 10;
   return (0.948 + 1.395 * ch) * (double)((waves + n_simd - 1) / n_simd);
 }
-static void l0_shape(uint64_t nd, uint32_t n_simd, bool g_free, uint32_t& G, uint32_t& C) {
-  const uint32_t cand[3][2] = {{g_free ? 16u : G, 4}, {g_free ? 16u : G, 8}, {14, 7}};
+// Round 6: with the group size free, every chunk C of
+// 5 .. 10 duties is a candidate too, as (G, C) = (C, C) -- one chunk per
+// group -- so the hexads can fill whole wave-slot rounds: the 20-step plan's
+// 200k duties take (10, 10) (2,000 waves: 2 rounds) instead of (14, 7) (2,858
+// waves: 3 rounds; +2.6 % at the driver shape, profiles/r06/shape), config
+// 3's 100k (10, 10) instead of (16, 4) (Miller 8.0 vs 9.4 ms).  Chunks of 13
+// and 16 duties were measured far off the model (a round of ~1,000 lone
+// waves: (16, 16) 20.4 ms vs (16, 8) 12.2 ms at 160k duties, (13, 13) 16.8
+// vs (14, 7) 11.0 ms at 125k: the C line loads of a step are not hidden by a
+// second wave), so C stops at L0_SHAPE_MAX_C.
+// `fits` (a replay's arenas, below) drops the candidates a launch cannot hold.
+static bool l0_fits_any(uint32_t, uint32_t) { return true; }
+static void l0_shape(uint64_t nd, uint32_t n_simd, bool g_free, uint32_t& G, uint32_t& C,
+                     const std::function<bool(uint32_t, uint32_t)>& fits) {
   C = 4;
   if (!TBG_L0_SHAPE || G < 8) return;
+  constexpr uint32_t L0_SHAPE_MAX_C = 10;
+  uint32_t cand[3 + L0_SHAPE_MAX_C][2] = {{g_free ? 16u : G, 4}, {g_free ? 16u : G, 8}, {14, 7}};
+  uint32_t n_cand = g_free ? 3u : 2u;
+  for (uint32_t c = 5; TBG_L0_SHAPE_WIDE && g_free && c <= L0_SHAPE_MAX_C; ++c) {
+    cand[n_cand][0] = c;
+    cand[n_cand][1] = c;
+    ++n_cand;
+  }
+  double best = 1e300;
   const uint32_t G0 = G;
-  double best = l0_shape_cost(nd, n_simd, G0, 4);
-  for (uint32_t k = 1; k < (g_free ? 3u : 2u); ++k) {
+  for (uint32_t k = 0; k < n_cand; ++k) {
+    if (!fits(cand[k][0], cand[k][1])) continue;
     const double cost = l0_shape_cost(nd, n_simd, cand[k][0], cand[k][1]);
-    if (cost < best) {
+    if (cost < best - 1e-9) {
       best = cost;
       G = cand[k][0];
       C = cand[k][1];
     }
   }
+  if (best == 1e300) G = G0;  // (nothing fits: the caller keeps its shapes)
 }
 // A launch of nd duties (a prefix of its slot's device batch) at (G, C) fits
 // the slot's arena, whose group / chunk sections were sized at submit for
@@ -708,7 +731,7 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   const bool l0 = G != 0 && np < (1u << 28) &&
                   (c->rlc_batch == TBG_RLC_L0_ON || (c->rlc_batch == TBG_RLC_L0_AUTO && c->invalid_ema < TBG_RLC_AUTO_L0));
   uint32_t C = c->rlc_chunk;
-  if (l0 && c->chunk_auto) l0_shape(nd, c->n_simd, c->rlc_auto && G == 16, G, C);
+  if (l0 && c->chunk_auto) l0_shape(nd, c->n_simd, c->rlc_auto && G == 16, G, C, l0_fits_any);
   if (C > G) C = G ? G : 1;
   const uint32_t ng = G ? (nd + G - 1) / G : 0;
   const uint32_t nch = G ? (G + C - 1) / C : 0;
@@ -1163,8 +1186,16 @@ int tbg_replay_plan(tbg_ctx* c, const tbg_ticket* tickets, const uint32_t* n_par
         nd += bs[k].n_duties;
         all_l0 = all_l0 && bs[k].rlc_batch && bs[k].rlc_group >= 8;
       }
+      // the cheapest shape every launch of the run can hold (round 6: the
+      // candidates that one of them cannot are skipped, not the reshape)
       uint32_t G = 16, C = 4;
-      if (all_l0) l0_shape(nd, c->n_simd, true, G, C);
+      auto fits_all = [&](uint32_t g, uint32_t ch) {
+        for (uint32_t k = k0; k < k1; ++k)
+          if (!l0_shape_fits(sl[k]->n_duties, sl[k]->B.rlc_group, sl[k]->B.rlc_chunk, bs[k].n_duties, g, ch))
+            return false;
+        return true;
+      };
+      if (all_l0) l0_shape(nd, c->n_simd, true, G, C, fits_all);
       for (uint32_t k = k0; k < k1 && all_l0; ++k)
         if (l0_shape_fits(sl[k]->n_duties, sl[k]->B.rlc_group, sl[k]->B.rlc_chunk, bs[k].n_duties, G, C)) {
           bs[k].rlc_group = G;

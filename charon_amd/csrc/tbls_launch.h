@@ -32,6 +32,11 @@ constexpr uint32_t PK_TAB = TBG_PK_W2 ? 8u : 2u;  // G1A entries per key in the 
 #ifndef TBG_L0_SHAPE
 #define TBG_L0_SHAPE 1
 #endif
+// 1 (round 6): one-chunk groups of 5 .. 10 duties are level-0 shape
+// candidates too; 0: (16, 4), (16, 8), (14, 7) only
+#ifndef TBG_L0_SHAPE_WIDE
+#define TBG_L0_SHAPE_WIDE 1
+#endif
 #ifndef TBG_FB_WINDOW
 #define TBG_FB_WINDOW 32768u
 #endif

@@ -2,7 +2,9 @@
 (tbls_engine.hip: l0_shape over their duties, applied where each slot's
 arena fits it).  Three slots of 16 caller batches of 2,500 3-of-4 DVs
 (40k duties each, submitted at (G, C) = (16, 4)) replayed as the bench's
-prefixes of 7 + 7 + 6 batches: 50k duties together take (14, 7).  Level 0
+prefixes of 7 + 7 + 6 batches: 50k duties together take the cheapest shape
+every launch's arena holds -- (14, 7), where (5, 5), cheaper, would need
+more groups than the (16, 4) arenas have (round 6).  Level 0
 must still PASS on the clean slots and FAIL on the slot holding one
 wrong-share partial, and every replayed batch must equal its known answer
 (the fallback levels run at the replay's shape too)."""
@@ -20,11 +22,13 @@ PREFIX = [7, 7, 6]
 
 def test_replay_plan_reshaped_launches():
     from charon_amd import engine as eng
-    from tests.test_gpu_shape import expected_shape
+    from tests.test_gpu_shape import expected_shape, shape_fits
     from tools.workload import make_batch
     n_cu = eng.device_cu_count(0)
     assert expected_shape(DVS * PER_SLOT, n_cu) == (16, 4)
-    assert expected_shape(DVS * sum(PREFIX), n_cu) == (14, 7)
+    assert expected_shape(DVS * sum(PREFIX), n_cu) == (5, 5)
+    fits = lambda g, c: all(shape_fits(DVS * PER_SLOT, 16, 4, DVS * n, g, c) for n in PREFIX)  # noqa: E731
+    assert expected_shape(DVS * sum(PREFIX), n_cu, fits=fits) == (14, 7)
     e = eng.Engine(0, slots=SLOTS)
     try:
         groups = [[make_batch(e, DVS, 3, 4, seed=9000 + 100 * s + k) for k in range(PER_SLOT)] for s in range(SLOTS)]
@@ -45,6 +49,7 @@ def test_replay_plan_reshaped_launches():
                 _known_answer(e.collect(t), x)
         assert [e.shape(ts[0])["chunk"] for ts in tickets] == [4, 4, 4]
         e.replay_plan([ts[0] for ts in tickets], PREFIX)
+        assert [(e.shape(ts[0])["group"], e.shape(ts[0])["chunk"]) for ts in tickets] == [(14, 7)] * 3
         assert e.level0(tickets[0][0]) == eng.L0_PASSED
         assert e.level0(tickets[1][0]) == eng.L0_FAILED
         assert e.level0(tickets[2][0]) == eng.L0_PASSED
@@ -61,17 +66,19 @@ def test_replay_prefix_keeps_shape_its_chunk_arena_cannot_hold():
     """a replay may only reshape a launch where EVERY
     group / chunk section of the slot's arena holds the new shape.  A slot
     submitted as 90k + 70k duties is sized at (16, 8) (20,000 chunks); its
-    90k-duty prefix alone would take (16, 4) -- 22,500 chunks, more than the
-    chunk lists and chunk values hold -- so the replay must keep (16, 8).
-    With 20 % invalid partials nearly every group fails level 0 and level 1,
-    so the chunk-level kernels write every chunk slot: the prefix must still
-    equal its known answer."""
+    90k-duty prefix takes the cheapest shape that arena holds -- never (16,
+    4) (22,500 chunks, more than the chunk lists and chunk values hold, the
+    overflow ADVICE r05 found), which the prefix alone would otherwise take.  With 20 % invalid partials nearly every
+    group fails level 0 and level 1, so the chunk-level kernels write every
+    chunk slot: the prefix must still equal its known answer."""
     from charon_amd import engine as eng
-    from tests.test_gpu_shape import expected_shape
+    from tests.test_gpu_shape import expected_shape, shape_fits
     from tools.workload import make_batch
     n_cu = eng.device_cu_count(0)
     assert expected_shape(160000, n_cu) == (16, 8)
-    assert expected_shape(90000, n_cu) == (16, 4)
+    assert not shape_fits(160000, 16, 8, 90000, 16, 4)
+    G, C = expected_shape(90000, n_cu, fits=lambda g, c: shape_fits(160000, 16, 8, 90000, g, c))
+    assert (G, C) != (16, 4)
     e = eng.Engine(0, slots=1, rlc_batch=eng.RLC_L0_ON)
     try:
         a = make_batch(e, 90000, 3, 4, seed=9901, inject=0.2)
@@ -82,10 +89,10 @@ def test_replay_prefix_keeps_shape_its_chunk_arena_cannot_hold():
         assert (e.shape(ta)["group"], e.shape(ta)["chunk"]) == (16, 8)
         assert e.level0(ta) == eng.L0_FAILED
         e.replay_plan([ta], [1])
-        # the launch ran at the submitted shape, over the prefix's duties
+        # the launch ran at the cheapest shape its arena holds, over the prefix's duties
         sh = e.shape(ta)
-        assert (sh["group"], sh["chunk"]) == (16, 8)
-        assert sh["chunks"] == -(-90000 // 16) * 2
+        assert (sh["group"], sh["chunk"]) == (G, C) and shape_fits(160000, 16, 8, 90000, G, C)
+        assert sh["chunks"] == -(-90000 // G) * -(-G // C)
         _known_answer(e.fetch(ta, a.n_dv, len(a.identifiers)), a)
     finally:
         e.close()
