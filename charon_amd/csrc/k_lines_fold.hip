@@ -15,10 +15,7 @@
 namespace tbg {
 
 template <int KIND>
-__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
-  // both lanes of a pair take the same branches; the fallback kinds run in
-  // passes of fb_window list positions from fb_base (launch_rlc_check)
-  const uint32_t k = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + (KIND == FOLD_GROUPS ? 0u : B.fb_base);
+__device__ __forceinline__ void lines_fold_one(const DevBatch& B, uint32_t k) {
   uint32_t* out;
   if (KIND == FOLD_GROUPS) {
     if (k >= (B.n_duties + B.rlc_group - 1) / B.rlc_group || B.grp_state[k] != GRP_LINES) return;
@@ -39,6 +36,23 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
   const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
   px_g2_lines(px_load(B.pend_pts[k]), nx, fp_from_const(G1_NEG_Y),
               out + (KIND == FOLD_GROUPS ? (size_t)LINES_WORDS * k : fb_slot(B, k)));
+}
+
+template <int KIND>
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_fold(DevBatch B) {
+  // both lanes of a pair take the same branches; the fallback kinds run in
+  // passes of fb_window list positions from fb_base (launch_rlc_check), a
+  // grid smaller than the pass looping over it (fb_pass_loop)
+  const uint32_t pr = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (KIND == FOLD_GROUPS) {
+    lines_fold_one<KIND>(B, pr);
+    return;
+  }
+  const uint32_t count = KIND == FOLD_CHUNKS ? B.counters[CNT_CHUNKS]
+                         : KIND == FOLD_CID  ? B.counters[CNT_CID]
+                         : KIND == FOLD_GID  ? B.counters[CNT_GID]
+                                             : B.counters[CNT_DUTIES];
+  fb_pass_loop(B, pr, (gridDim.x * blockDim.x) >> 1, count, [&](uint32_t k) { lines_fold_one<KIND>(B, k); });
 }
 
 void launch_lines_fold(const DevBatch& B, int kind, uint32_t max_entries, hipStream_t st) {

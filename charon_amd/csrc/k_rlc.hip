@@ -618,10 +618,11 @@ __global__ void TBG_LAUNCH k_rlc_ident_lines(DevBatch B) {
 // Level 2b check: one hexad per entry computes A'_d and tests A_d^w == A'_d.
 // Found -> partial w invalid, the others valid; not found -> level 3.
 __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_ident_check(DevBatch B) {
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = hex_slot(t) + B.fb_base;
-  if (hex_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_DUTIES] || !fb_in_pass(B, k)) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (hex_slot(t) == 0xFFFFFFFFu) return;
   const bool lead = hex_lead();
+  const uint32_t per = (gridDim.x * (blockDim.x / 64u) * 10u);
+  fb_pass_loop(B, hex_slot(t), per, B.counters[CNT_DUTIES], [&](uint32_t k) {
   const uint32_t entry = B.id_list[k], d = entry & ~ID_DEGENERATE;
   uint32_t found = 0;
   if (!(entry & ID_DEGENERATE)) {
@@ -643,6 +644,7 @@ __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_rlc_ident_check(DevBatch B) {
     if (!rlc_candidate(B, i)) continue;
     B.partial_status[i] = ++w == found ? TBG_PS_INVALID : TBG_PS_VALID;
   }
+  });
 }
 
 // ------------------------------------------------------------ level 1g
@@ -832,46 +834,57 @@ __global__ void TBG_LAUNCH k_list_all_partials(DevBatch B, const int32_t* pk_sta
 // folded in.  (One lane per partial: 2.6 ms of latency per 16-batch launch
 // at 1 % invalid against 1.4 ms, profiles/r04/merge/.)
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_lines_sig_list(DevBatch B) {
-  const uint32_t k = ((blockIdx.x * blockDim.x + threadIdx.x) >> 1) + B.fb_base;  // (pair-uniform branches)
-  if (k >= B.counters[CNT_PARTIALS] || !fb_in_pass(B, k)) return;
-  const uint32_t i = B.part_list[k];
-  const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
-  Aff<Fp2x> q = px_load(B.sig_aff[i]);
-  q = {f_reduce(q.x), f_reduce(q.y)};  // decoded coordinates may be up to 16p (a negated root)
-  px_g2_lines(q, nx, fp_from_const(G1_NEG_Y), B.sig_lines + fb_slot(B, k));
+  // (pair-uniform branches; a grid smaller than the pass loops: fb_pass_loop)
+  fb_pass_loop(B, (blockIdx.x * blockDim.x + threadIdx.x) >> 1, (gridDim.x * blockDim.x) >> 1,
+               B.counters[CNT_PARTIALS], [&](uint32_t k) {
+    const uint32_t i = B.part_list[k];
+    const Fp nx = fp_reduce(fp_neg(fp_from_const(G1_X)));
+    Aff<Fp2x> q = px_load(B.sig_aff[i]);
+    q = {f_reduce(q.x), f_reduce(q.y)};  // decoded coordinates may be up to 16p (a negated root)
+    px_g2_lines(q, nx, fp_from_const(G1_NEG_Y), B.sig_lines + fb_slot(B, k));
+  });
 }
 
 // Level 3 check: one hexad per listed partial, the exact CoreVerify.
+// (grid-stride over the pass: hexad slots per grid = 10 per wave)
+TBG_DEV uint32_t hex_grid_slots() { return gridDim.x * (blockDim.x / 64u) * 10u; }
+
 __global__ void TBG_LAUNCH_N(TBG_HEX_WAVES) k_verify_list(DevBatch B, const G1A* pk_aff) {
-  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = hex_slot(t) + B.fb_base;
-  if (hex_slot(t) == 0xFFFFFFFFu || k >= B.counters[CNT_PARTIALS] || !fb_in_pass(B, k)) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (hex_slot(t) == 0xFFFFFFFFu) return;
   const bool lead = hex_lead();
-  uint32_t i = B.part_list[k];
-  uint32_t m = B.duty_msg[B.partial_duty[i]];
-  if (B.h_status[m] != 0) {
-    if (lead) B.partial_status[i] = TBG_PS_INVALID;
-    return;
-  }
-  G1A pk = pk_aff[B.pubkey_ids[i]];
-  Fp nx = fp_reduce(fp_neg(pk.x));
-  const uint32_t* ls = B.sig_lines + fb_slot(B, k);
-  const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * m;
-  Fp4h f = hex_miller([&](Fp4h x, int idx) { return hex_line_at(hex_line_folded(x, ls, idx), lh, idx, nx, pk.y); });
-  f = hex_final_exp_in(hex_conj(f));
-  const bool ok = hex_is_one(f);
-  if (lead) B.partial_status[i] = ok ? TBG_PS_VALID : TBG_PS_INVALID;
+  fb_pass_loop(B, hex_slot(t), hex_grid_slots(), B.counters[CNT_PARTIALS], [&](uint32_t k) {
+    uint32_t i = B.part_list[k];
+    uint32_t m = B.duty_msg[B.partial_duty[i]];
+    if (B.h_status[m] != 0) {
+      if (lead) B.partial_status[i] = TBG_PS_INVALID;
+      return;
+    }
+    G1A pk = pk_aff[B.pubkey_ids[i]];
+    Fp nx = fp_reduce(fp_neg(pk.x));
+    const uint32_t* ls = B.sig_lines + fb_slot(B, k);
+    const uint32_t* lh = B.h_lines + (size_t)LINES_WORDS * m;
+    Fp4h f = hex_miller([&](Fp4h x, int idx) { return hex_line_at(hex_line_folded(x, ls, idx), lh, idx, nx, pk.y); });
+    f = hex_final_exp_in(hex_conj(f));
+    const bool ok = hex_is_one(f);
+    if (lead) B.partial_status[i] = ok ? TBG_PS_VALID : TBG_PS_INVALID;
+  });
 }
 
 // The fallback levels' list positions [0, max_entries) in passes of
 // B.fb_window (the line buffer's capacity; 0: one pass), in stream order.
+// body(P, n): n = the list positions the pass's grids cover -- all of the
+// pass below B.fb_full, else FB_SMALL (the pass kernels that may run small
+// loop over the rest: fb_pass_loop; the others take n = the pass).
+constexpr uint32_t FB_SMALL = 640;  // 64 hexad waves, 20 pair waves
 template <class F>
-static void fb_passes(const DevBatch& B, uint32_t max_entries, F&& body) {
+static void fb_passes(const DevBatch& B, uint32_t max_entries, F&& body, bool may_shrink = false) {
   const uint32_t W = B.fb_window ? B.fb_window : max_entries;
   for (uint32_t base = 0; base < max_entries; base += W) {
     DevBatch P = B;
     P.fb_base = base;
-    body(P, max_entries - base < W ? max_entries - base : W);
+    const uint32_t n = max_entries - base < W ? max_entries - base : W;
+    body(P, may_shrink && base > 0 && base >= B.fb_full && n > FB_SMALL ? FB_SMALL : n);  // (pass 0 always full)
   }
 }
 
@@ -974,14 +987,14 @@ void launch_rlc_check(const DevBatch& B, const G1A* pk_aff, const G1A* xpk_aff, 
       fb_passes(B, B.n_duties, [&](const DevBatch& P, uint32_t n) {
         launch_lines_fold(P, FOLD_IDENT, n, st);
         TBG_KLAUNCH(k_rlc_ident_check, grid_for(hex_threads(n)), dim3(kBlock), st, P);
-      });
+      }, true);
     }
   }
   if (B.n_partials) {
     fb_passes(B, B.n_partials, [&](const DevBatch& P, uint32_t n) {
       TBG_KLAUNCH(k_lines_sig_list, grid_for(2 * n), dim3(kBlock), st, P);
       TBG_KLAUNCH(k_verify_list, grid_for(hex_threads(n)), dim3(kBlock), st, P, pk_aff);
-    });
+    }, true);
   }
 }
 

@@ -967,6 +967,15 @@ int tbg_submit_group(tbg_ctx* c, const tbg_batch* const* bs, uint32_t n_batches,
   B.id_p = (G1A*)(dw + w_idp);
   B.id_lines = B.sig_lines;
   B.fb_window = fb_w;
+  {
+    // full-grid passes of the duty / partial lists: those the collected
+    // batches' invalid share makes likely (10x margin), every pass for the
+    // per-partial schedule
+    const double share = std::min(1.0, 10.0 * c->invalid_ema);
+    const uint64_t expect = (uint64_t)((double)np * share);
+    B.fb_full = (!TBG_FB_EXPECT || G == 0 || fb_w == 0) ? 0xFFFFFFFFu
+                                      : (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (expect / fb_w + 1) * (uint64_t)fb_w);
+  }
   B.fb_base = 0;
   B.partial_status = (int32_t*)(dw + w_pst);
   B.duty_status = (int32_t*)(dw + w_dst);
@@ -1669,6 +1678,7 @@ int tbg_fast_aggregate_verify(tbg_ctx* c, const uint32_t* pubkey_ids, const uint
   B.partial_status = (int32_t*)a.sec(4ull * n);
   B.duty_status = (int32_t*)a.sec(4ull * n);
   B.rlc_group = 0;
+  B.fb_full = 0xFFFFFFFFu;
   if (mb) HIP_TRY(hipMemcpyAsync(d_msgs, msgs, mb, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(d_moff, msg_off, 4ull * (n + 1), hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(d_iota, iota.data(), 4ull * (n + 1), hipMemcpyHostToDevice, st));

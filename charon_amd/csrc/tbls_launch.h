@@ -40,6 +40,11 @@ constexpr uint32_t PK_TAB = TBG_PK_W2 ? 8u : 2u;  // G1A entries per key in the 
 #ifndef TBG_FB_WINDOW
 #define TBG_FB_WINDOW 32768u
 #endif
+// 1 (round 6): the duty / partial list passes beyond the expected list
+// length launch small grids that loop (DevBatch::fb_full); 0: every pass full
+#ifndef TBG_FB_EXPECT
+#define TBG_FB_EXPECT 1
+#endif
 
 // Minimum waves per SIMD requested from the register allocator (1 lets a
 // kernel use all 512 / 2 = 256 VGPRs at two waves per SIMD; 3 caps it at
@@ -135,6 +140,13 @@ struct DevBatch {
   // level writes (launch_rlc_check) -- a slot's HBM no longer scales with the
   // worst-case list length (22.8 KB per partial of every batch).
   uint32_t fb_window, fb_base;
+  // Passes of the duty (level 2b) and partial (level 3) lists start full grids
+  // only below fb_full list positions (the list lengths the collected batches'
+  // invalid share makes likely); later passes launch a few waves that loop
+  // over the pass (k_verify_list, k_lines_sig_list, k_rlc_ident_check,
+  // k_lines_fold), so a clean batch does not dispatch ~80k empty waves of 20
+  // partial passes per 16-batch launch (round 6).  UINT32_MAX: every pass full.
+  uint32_t fb_full;
   uint32_t* id_lines;     // lines of sum w_i r_i sig_i by level-2b position: aliases sig_lines,
                           // which level 3 only fills after level 2b has consumed them
   // level 0 (k_msm.hip, k_rlc.hip): the whole device batch as ONE RLC check,
@@ -264,6 +276,17 @@ enum FoldKind : int { FOLD_GROUPS = 0, FOLD_CHUNKS = 1, FOLD_CID = 2, FOLD_IDENT
 // Fallback list position k in the current pass, and its slot in the line buffer.
 TBG_HD bool fb_in_pass(const DevBatch& B, uint32_t k) { return B.fb_window == 0 || k - B.fb_base < B.fb_window; }
 TBG_HD size_t fb_slot(const DevBatch& B, uint32_t k) { return (size_t)LINES_WORDS * (k - B.fb_base); }
+// The list positions of the current pass, from `first` in steps of `stride`
+// (a grid smaller than the pass loops): stops at the list's end or the pass's.
+template <class F>
+TBG_HD void fb_pass_loop(const DevBatch& B, uint32_t first, uint32_t stride, uint32_t count, F&& body) {
+  const uint32_t w = B.fb_window ? B.fb_window : 0xFFFFFFFFu;
+  for (uint32_t s = first; s < w; s += stride) {
+    const uint32_t k = B.fb_base + s;
+    if (k >= count) break;
+    body(k);
+  }
+}
 
 // 1: every VERIFY_AGGREGATE chain aggregates speculatively and redoes only
 // the duties with an invalid partial; 0 (default): speculate only while level
