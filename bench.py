@@ -204,7 +204,7 @@ def work_model():
 # Stages of the kernel chain (tbg_last_timings order) and their kernels.
 STAGE_KERNELS = {
     "decode": ["k_decode_sigs", "k_sgb_sort", "k_sgb_bucket", "k_sgb_fold", "k_sgb_combine", "k_sgb_test", "k_subgroup_sigs"],
-    "hash": ["k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
+    "hash": ["k_hash_map", "k_hash_sswu", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"],
     "combine": ["k_rlc_g1_l0", "k_msm_bucket", "k_msm_bucket_part", "k_msm_tree", "k_msm_tree_final", "k_msm_scan", "k_msm_scatter",
                 "k_rlc_duty_sum<DSUM_L0_P>", "k_rlc_duty_sum<DSUM_BOTH>", "k_rlc_duty_sum<DSUM_FALLBACK_S>",
                 "k_l0_lines", "k_rlc_partial2", "k_rlc_group_lines", "k_lines_fold<FOLD_GROUPS>",

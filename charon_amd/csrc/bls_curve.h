@@ -307,9 +307,12 @@ enum DecodeStatus : int32_t {
 // 96-byte ZCash compressed G2 -> affine (Montgomery).  INL = true runs the
 // subgroup check's doublings inline (kernel callers); SUBGROUP = false leaves
 // the subgroup check to the caller (k_decode_sigs hands it to the lane-pair
-// kernel k_subgroup_sigs, bls_pair.h).
-template <bool INL, bool SUBGROUP = true>
-TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out) {
+// kernel k_subgroup_sigs, bls_pair.h).  INL also takes the square root
+// inline, its input kept by `keep` (bls_tower.h); x goes to out.x before the
+// root and is read back from there (a kernel decoding into its output slot
+// keeps neither value in registers across the exponentiations).
+template <bool INL, bool SUBGROUP = true, class Keep = RegKeep>
+TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out, Keep keep = Keep{}) {
   uint32_t c_flag = (b[0] >> 7) & 1, i_flag = (b[0] >> 6) & 1, s_flag = (b[0] >> 5) & 1;
   if (!c_flag) return DEC_ERR_FLAGS;
   uint8_t hi[48];
@@ -324,12 +327,12 @@ TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out) {
     return (s_flag == 0 && o == 0) ? DEC_IDENTITY : DEC_ERR_FLAGS;
   }
   if (!lt0 || !lt1) return DEC_ERR_FIELD;
-  Fp2 x = {fp_to_mont(x0), fp_to_mont(x1)};
-  Fp2 rhs = fp2_reduce(fp2_add(fp2_mul(fp2_sqr(x), x), fp2_from_const(B2_M)));
-  Fp2 y;
-  if (!fp2_sqrt(rhs, y)) return DEC_ERR_NOT_ON_CURVE;
-  if ((uint32_t)fp2_lex_largest(y) != s_flag) y = fp2_reduce(fp2_neg(y));
+  const Fp2 x = {fp_to_mont(x0), fp_to_mont(x1)};
   out.x = x;
+  const Fp2 rhs = fp2_reduce(fp2_add(fp2_mul(fp2_sqr(x), x), fp2_from_const(B2_M)));
+  Fp2 y;
+  if (!(INL ? fp2_sqrt_in<3>(rhs, y, keep) : fp2_sqrt(rhs, y))) return DEC_ERR_NOT_ON_CURVE;
+  if ((uint32_t)fp2_lex_largest(y) != s_flag) y = fp2_reduce(fp2_neg(y));
   out.y = y;
   if (SUBGROUP && !(INL ? g2_in_subgroup_aff_in(out) : g2_in_subgroup(jac_from_aff(out)))) return DEC_ERR_SUBGROUP;
   return DEC_OK;

@@ -436,8 +436,10 @@ TBG_HD Fp fp_to_mont(const Fp& a) {
 // registers: k_hash_map's square roots take it (7.2 -> 6.8 ms per 16-batch
 // launch), k_decode_sigs lost 13 % with it and keeps width 3
 // (profiles/r04/pow/).
+// (_in: the inline body, for kernels that keep the whole chain in registers
+// -- k_hash_sswu; fp_pow_const: out of line.)
 template <int NBITS, const uint32_t (&WD)[12], int WIN = 3>
-TBG_NI Fp fp_pow_const(const Fp& a) {
+TBG_HD Fp fp_pow_const_in(const Fp& a) {
   static_assert(WIN == 3 || WIN == 4, "window width");
   const Fp a2 = fp_sqr(a);
   const Fp t1 = a, t3 = fp_mul(t1, a2), t5 = fp_mul(t3, a2), t7 = fp_mul(t5, a2);
@@ -476,6 +478,10 @@ TBG_NI Fp fp_pow_const(const Fp& a) {
     i -= L;
   }
   return r;
+}
+template <int NBITS, const uint32_t (&WD)[12], int WIN = 3>
+TBG_NI Fp fp_pow_const(const Fp& a) {
+  return fp_pow_const_in<NBITS, WD, WIN>(a);
 }
 
 // Fermat: a^(p-2), ~380 squarings + ~95 products in one dependent chain

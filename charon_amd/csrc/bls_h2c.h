@@ -94,7 +94,7 @@ TBG_HD void sha256_dst_prime(Sha256& s) {
 }
 
 // expand_message_xmd(msg, DST, 256): out[256]  (byte-stream reference form;
-// the kernels use expand_message_xmd_256w below)
+// the kernels use the word form of hash_to_field_fp2 below)
 TBG_NI void expand_message_xmd_256(const uint8_t* msg, uint32_t msg_len, uint8_t* out) {
   Sha256 s;
   sha256_init(s);
@@ -177,63 +177,6 @@ TBG_HD uint32_t b0_stream_byte(const uint8_t* msg, uint32_t L, uint32_t p) {
   return p == L + 3 + DST_LEN + 1 ? 0x80u : 0u;
 }
 
-// out[64]: the 256 output bytes as big-endian words.
-TBG_HD void expand_message_xmd_256w(const uint8_t* msg, uint32_t L, uint32_t (&out)[64]) {
-  uint32_t h[8], w[16];
-  sha256_iv(h);
-#pragma unroll
-  for (int k = 0; k < 16; ++k) w[k] = 0;
-  sha256_compress(h, w);  // Z_pad: one block of zeros
-  const uint32_t tail = L + 3 + DST_LEN + 1;  // bytes after Z_pad, before the padding
-  const uint32_t nb = (tail + 1 + 8 + 63) / 64;
-  const uint64_t bits = 8ull * (64 + tail);
-#pragma unroll 1
-  for (uint32_t blk = 0; blk < nb; ++blk) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t p = 64 * blk + 4 * k;
-      w[k] = (b0_stream_byte(msg, L, p) << 24) | (b0_stream_byte(msg, L, p + 1) << 16) |
-             (b0_stream_byte(msg, L, p + 2) << 8) | b0_stream_byte(msg, L, p + 3);
-    }
-    if (blk == nb - 1) {
-      w[14] = (uint32_t)(bits >> 32);
-      w[15] = (uint32_t)bits;
-    }
-    sha256_compress(h, w);
-  }
-  uint32_t b0[8], bi[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    b0[k] = h[k];
-    bi[k] = 0;  // b_1 = H(b_0 || 1 || DST_prime) = H(strxor(b_0, 0) || ...)
-  }
-#pragma unroll 1
-  for (uint32_t i = 1; i <= 8; ++i) {
-    // block 1: strxor(b_0, b_(i-1)) || I2OSP(i, 1) || DST_prime[0 .. 31)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) w[k] = b0[k] ^ bi[k];
-    w[8] = (i << 24) | (dstp_byte(0) << 16) | (dstp_byte(1) << 8) | dstp_byte(2);
-#pragma unroll
-    for (int k = 9; k < 16; ++k) w[k] = dstp_word(3 + 4 * (k - 9));
-    sha256_iv(h);
-    sha256_compress(h, w);
-    // block 2: DST_prime[31 .. 44) || 0x80 || 0... || bit length 77 * 8
-    w[0] = dstp_word(31);
-    w[1] = dstp_word(35);
-    w[2] = dstp_word(39);
-    w[3] = (dstp_byte(43) << 24) | 0x800000u;
-#pragma unroll
-    for (int k = 4; k < 15; ++k) w[k] = 0;
-    w[15] = 77 * 8;
-    sha256_compress(h, w);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      bi[k] = h[k];
-      out[8 * (i - 1) + k] = h[k];
-    }
-  }
-}
-
 // 32 big-endian bytes -> 14 limbs (value < 2^256)
 TBG_HD Fp limbs_from_be32(const uint8_t* b) {
   Fp r = fp_zero();
@@ -276,13 +219,72 @@ TBG_HD Fp fp_from_be_words16_mod(const uint32_t* w) {
   return fp_mul2(hi, ca, lo, cb);
 }
 
-TBG_HD void hash_to_field_fp2(const uint8_t* msg, uint32_t msg_len, Fp2& u0, Fp2& u1) {
-  uint32_t uni[64];
-  expand_message_xmd_256w(msg, msg_len, uni);
-  u0.c0 = fp_from_be_words16_mod(uni);
-  u0.c1 = fp_from_be_words16_mod(uni + 16);
-  u1.c0 = fp_from_be_words16_mod(uni + 32);
-  u1.c1 = fp_from_be_words16_mod(uni + 48);
+// expand_message_xmd's b_1 .. b_8 in pairs: pair k (b_(2k+1) || b_(2k+2)) is
+// the 16 words of one hash_to_field element, converted as soon as it is
+// complete (a per-pair loop keeps every word index static: no 64-word array
+// in scratch).
+TBG_HD void hash_to_field_fp2(const uint8_t* msg, uint32_t L, Fp2& u0, Fp2& u1) {
+  uint32_t h[8], w[16];
+  sha256_iv(h);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = 0;
+  sha256_compress(h, w);  // Z_pad: one block of zeros
+  const uint32_t tail = L + 3 + DST_LEN + 1;
+  const uint32_t nb = (tail + 1 + 8 + 63) / 64;
+  const uint64_t bits = 8ull * (64 + tail);
+#pragma unroll 1
+  for (uint32_t blk = 0; blk < nb; ++blk) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t p = 64 * blk + 4 * k;
+      w[k] = (b0_stream_byte(msg, L, p) << 24) | (b0_stream_byte(msg, L, p + 1) << 16) |
+             (b0_stream_byte(msg, L, p + 2) << 8) | b0_stream_byte(msg, L, p + 3);
+    }
+    if (blk == nb - 1) {
+      w[14] = (uint32_t)(bits >> 32);
+      w[15] = (uint32_t)bits;
+    }
+    sha256_compress(h, w);
+  }
+  uint32_t b0[8], bi[8], grp[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    b0[k] = h[k];
+    bi[k] = 0;
+  }
+  Fp e[4] = {fp_zero(), fp_zero(), fp_zero(), fp_zero()};
+#pragma unroll 1
+  for (uint32_t pr = 0; pr < 4; ++pr) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint32_t i = 2 * pr + half + 1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = b0[k] ^ bi[k];
+      w[8] = (i << 24) | (dstp_byte(0) << 16) | (dstp_byte(1) << 8) | dstp_byte(2);
+#pragma unroll
+      for (int k = 9; k < 16; ++k) w[k] = dstp_word(3 + 4 * (k - 9));
+      sha256_iv(h);
+      sha256_compress(h, w);
+      w[0] = dstp_word(31);
+      w[1] = dstp_word(35);
+      w[2] = dstp_word(39);
+      w[3] = (dstp_byte(43) << 24) | 0x800000u;
+#pragma unroll
+      for (int k = 4; k < 15; ++k) w[k] = 0;
+      w[15] = 77 * 8;
+      sha256_compress(h, w);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bi[k] = h[k];
+        grp[8 * half + k] = h[k];
+      }
+    }
+    const Fp v = fp_from_be_words16_mod(grp);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = fp_select(pr == (uint32_t)k, v, e[k]);
+  }
+  u0 = Fp2{e[0], e[1]};
+  u1 = Fp2{e[2], e[3]};
 }
 
 // the byte-stream reference form (host tests compare the two)
@@ -326,52 +328,72 @@ TBG_NI G2J map_to_curve_g2(const Fp2& u) {
 }
 
 // 3-isogeny E2' -> E2 of an affine point: x = x_num / x_den, y = y' y_num /
-// y_den, as Jacobian (X, Y, Z) = (x_num x_den y_den^2, y' y_num x_den^3 y_den^2,
-// x_den y_den).
-TBG_NI G2J iso3_to_jac(const Fp2& x, const Fp2& y) {
-  Fp2 xx = fp2_sqr(x), xxx = fp2_mul(xx, x);
-  Fp2 xnum = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_from_const(ISO_K13), xxx), fp2_mul(fp2_from_const(ISO_K12), xx)),
-                                fp2_add(fp2_mul(fp2_from_const(ISO_K11), x), fp2_from_const(ISO_K10))));
-  Fp2 xden = fp2_reduce(fp2_add(fp2_add(xx, fp2_mul(fp2_from_const(ISO_K21), x)), fp2_from_const(ISO_K20)));
-  Fp2 ynum = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_from_const(ISO_K33), xxx), fp2_mul(fp2_from_const(ISO_K32), xx)),
-                                fp2_add(fp2_mul(fp2_from_const(ISO_K31), x), fp2_from_const(ISO_K30))));
-  Fp2 yden = fp2_reduce(fp2_add(fp2_add(xxx, fp2_mul(fp2_from_const(ISO_K42), xx)),
-                                fp2_add(fp2_mul(fp2_from_const(ISO_K41), x), fp2_from_const(ISO_K40))));
-  Fp2 yden2 = fp2_sqr(yden);
+// y_den, as Jacobian (X, Y, Z) = (x_num y_den Z, y' y_num x_den Z^2, Z) with
+// Z = x_den y_den (X / Z^2 = x_num / x_den, Y / Z^3 = y' y_num / y_den).  The
+// four polynomials by Horner's rule in x (K13 and K33 are in Fp): 15 Fp2
+// products, two of them by an Fp constant, and few live
+// values (the output's coordinates are written as soon as they are formed --
+// Out is a G2J in registers, or a kernel's slot in memory).
+template <class Out>
+TBG_HD void iso3_emit(const Fp2& x, const Fp2& y, Out& r) {
+  auto hstep = [&](const Fp2& acc, const Fp2Const& k) { return fp2_reduce(fp2_add(fp2_mul(acc, x), fp2_from_const(k))); };
+  const Fp2 xden = hstep(fp2_reduce(fp2_add(x, fp2_from_const(ISO_K21))), ISO_K20);
+  const Fp2 yden = hstep(hstep(fp2_reduce(fp2_add(x, fp2_from_const(ISO_K42))), ISO_K41), ISO_K40);
+  const Fp2 z = fp2_mul(xden, yden);
+  r.Z = z;
+  const Fp2 xnum = hstep(hstep(fp2_reduce(fp2_add(fp2_mul_fp(x, fp_from_const(ISO_K13.c0)), fp2_from_const(ISO_K12))), ISO_K11),
+                         ISO_K10);
+  r.X = fp2_mul(fp2_mul(xnum, yden), z);
+  const Fp2 ynum = hstep(hstep(fp2_reduce(fp2_add(fp2_mul_fp(x, fp_from_const(ISO_K33.c0)), fp2_from_const(ISO_K32))), ISO_K31),
+                         ISO_K30);
+  r.Y = fp2_mul(fp2_mul(fp2_mul(y, ynum), xden), fp2_sqr(z));
+}
+TBG_HD G2J iso3_to_jac_in(const Fp2& x, const Fp2& y) {
   G2J r;
-  r.Z = fp2_mul(xden, yden);
-  r.X = fp2_mul(fp2_mul(xnum, xden), yden2);
-  Fp2 xden3 = fp2_mul(fp2_sqr(xden), xden);
-  r.Y = fp2_mul(fp2_mul(fp2_mul(y, ynum), xden3), yden2);
+  iso3_emit(x, y, r);
   return r;
 }
+TBG_NI G2J iso3_to_jac(const Fp2& x, const Fp2& y) { return iso3_to_jac_in(x, y); }
 
 // Root of a or of Z a, whichever is a square (a non-square in Fp2 times the
 // non-square Z is a square), from one Fp exponentiation on the norm plus one
 // for the root (norm method, as fp2_sqrt).  sq reports which.  False on the
 // inputs the closed form does not cover (a.c1 == 0 or (Z a).c1 == 0), which
 // the caller routes to the reference path.
-TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) {
+// (RegKeep, the keeper of fp2_sqrt_or_z_in's input: bls_tower.h)
+// k_hash_sswu's exponentiation window: width 4 (eight odd powers) spills 27
+// VGPRs there and still runs 4.99 vs 5.24 ms per 160k-message launch at
+// width 3 (profiles/r06/hash).
+#ifndef TBG_SSWU_WIN
+#define TBG_SSWU_WIN 4
+#endif
+constexpr int SSWU_WIN = TBG_SSWU_WIN;
+template <int WIN = 4, class Keep = RegKeep>
+TBG_HD bool fp2_sqrt_or_z_in(const Fp2& a_in, Fp2& root, bool& sq, Keep keep = Keep{}) {
   Fp2 a = fp2_reduce(a_in);
-  Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
-  Fp gamma = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS, 4>(norm);
-  sq = fp_eq(fp_sqr(gamma), norm);
+  keep.put(a);
+  Fp gamma = fp_pow_const_in<EXP_SQRT_BITS, EXP_SQRT_WORDS, WIN>(fp_mul2(a.c0, a.c0, a.c1, a.c1));
+  a = keep.get();
+  sq = fp_eq(fp_sqr(gamma), fp_mul2(a.c0, a.c0, a.c1, a.c1));
   if (!sq) {
     // gamma^2 = -norm(a); K gamma is a root of norm(Z) norm(a) = norm(Z a)
     a = fp2_reduce(fp2_mul(fp2_from_const(SSWU_Z), a));
     gamma = fp_mul(gamma, fp_from_const(SSWU_SQRT_NEG_NORM_Z));
   }
   if (fp_is_zero(a.c1)) return false;
-  Fp inv2 = fp_from_const(INV2_M);
-  Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);
-  Fp t = fp_pow_const<EXP_PM3D4_BITS, EXP_PM3D4_WORDS, 4>(delta);  // delta^((p-3)/4)
-  Fp x0 = fp_mul(delta, t);
-  Fp h = fp_mul(fp_mul(a.c1, t), inv2);
-  bool res = fp_eq(fp_sqr(x0), delta);
-  Fp2 r = {fp_select(res, x0, h), fp_select(res, h, fp_reduce(fp_neg(x0)))};
+  keep.put(a);
+  const Fp inv2 = fp_from_const(INV2_M);
+  const Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);
+  const Fp t = fp_pow_const_in<EXP_PM3D4_BITS, EXP_PM3D4_WORDS, WIN>(delta);  // delta^((p-3)/4)
+  a = keep.get();
+  const Fp x0 = fp_mul(delta, t);
+  const Fp h = fp_mul(fp_mul(a.c1, t), inv2);
+  const bool res = fp_eq(fp_sqr(x0), delta);
+  const Fp2 r = {fp_select(res, x0, h), fp_select(res, h, fp_reduce(fp_neg(x0)))};
   root = r;
   return fp2_eq(fp2_sqr(r), a);
 }
+TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) { return fp2_sqrt_or_z_in(a_in, root, sq); }
 
 // SSWU of both hash_to_field outputs with uniform control flow: one Fp2
 // inversion for the two denominators (Montgomery's trick) and one square
@@ -383,37 +405,52 @@ TBG_NI bool fp2_sqrt_or_z(const Fp2& a_in, Fp2& root, bool& sq) {
 // workgroup (k_hash_map, bls_batchinv.h): sswu_pair_den forms the product dd
 // of the two denominators, sswu_pair_finish takes di = 1 / dd.
 struct SswuPair {
-  Fp2 zu2[2], den[2];
+  Fp2 den[2];
 };
+// den = (Z u^2)^2 + Z u^2 of one map
+TBG_HD Fp2 sswu_den(const Fp2& u) {
+  const Fp2 zu2 = fp2_reduce(fp2_mul(fp2_from_const(SSWU_Z), fp2_sqr(u)));
+  return fp2_reduce(fp2_add(fp2_sqr(zu2), zu2));
+}
 TBG_HD Fp2 sswu_pair_den(const Fp2& u0, const Fp2& u1, SswuPair& w) {
-  const Fp2 Z = fp2_from_const(SSWU_Z);
-  const Fp2* u[2] = {&u0, &u1};
-  for (int j = 0; j < 2; ++j) {
-    w.zu2[j] = fp2_reduce(fp2_mul(Z, fp2_sqr(*u[j])));
-    w.den[j] = fp2_reduce(fp2_add(fp2_sqr(w.zu2[j]), w.zu2[j]));
-  }
+  w.den[0] = sswu_den(u0);
+  w.den[1] = sswu_den(u1);
   return fp2_reduce(fp2_mul(w.den[0], w.den[1]));
+}
+// x1 = -B/A (1 + 1/den) of one map from its inverse denominator.
+TBG_HD Fp2 sswu_x1(const Fp2& inv) {
+  return fp2_mul(fp2_from_const(SSWU_NEG_B_OVER_A), fp2_reduce(fp2_add(fp2_one(), inv)));
+}
+// One map from its u and x1 (the second half of k_hash.hip's split), in
+// three steps a kernel can keep apart: g(x1); the root of g(x1) or of Z g(x1)
+// (fp2_sqrt_or_z_in); x, y (Z u^2 recomputed, as sswu_pair_den forms it).
+TBG_HD Fp2 sswu_gx(const Fp2& x1) {
+  const Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B);
+  return fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_sqr(x1), x1), fp2_mul(A, x1)), B));
+}
+TBG_HD void sswu_xy(const Fp2& u, const Fp2& x1, const Fp2& r, bool sq, Fp2& x, Fp2& y) {
+  const Fp2 Z = fp2_from_const(SSWU_Z);
+  const Fp2 u2 = fp2_sqr(u);
+  x = sq ? x1 : fp2_mul(fp2_reduce(fp2_mul(Z, u2)), x1);
+  y = sq ? r : fp2_mul(fp2_mul(Z, fp2_mul(u2, u)), r);
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_reduce(fp2_neg(y));
+}
+// ... composed; false on the exceptional inputs fp2_sqrt_or_z does not cover
+TBG_HD bool sswu_map_x1(const Fp2& u, const Fp2& x1, G2J& q) {
+  Fp2 r, x, y;
+  bool sq;
+  if (!fp2_sqrt_or_z_in<SSWU_WIN>(sswu_gx(x1), r, sq)) return false;  // (k_hash_sswu's window width)
+  sswu_xy(u, x1, r, sq, x, y);
+  iso3_emit(x, y, q);
+  return true;
 }
 TBG_NI void sswu_pair_finish(const Fp2& u0, const Fp2& u1, const SswuPair& w, bool ok, const Fp2& di, G2J& q0,
                              G2J& q1) {
-  const Fp2 A = fp2_from_const(SSWU_A), B = fp2_from_const(SSWU_B), Z = fp2_from_const(SSWU_Z);
   const Fp2* u[2] = {&u0, &u1};
   Fp2 inv[2] = {fp2_mul(w.den[1], di), fp2_mul(w.den[0], di)};
   G2J* out[2] = {&q0, &q1};
-  for (int j = 0; j < 2 && ok; ++j) {
-    Fp2 x1 = fp2_mul(fp2_from_const(SSWU_NEG_B_OVER_A), fp2_reduce(fp2_add(fp2_one(), inv[j])));
-    Fp2 gx1 = fp2_reduce(fp2_add(fp2_add(fp2_mul(fp2_sqr(x1), x1), fp2_mul(A, x1)), B));
-    Fp2 r;
-    bool sq;
-    if (!fp2_sqrt_or_z(gx1, r, sq)) {
-      ok = false;
-      break;
-    }
-    Fp2 x = sq ? x1 : fp2_mul(w.zu2[j], x1);
-    Fp2 y = sq ? r : fp2_mul(fp2_mul(Z, fp2_mul(fp2_sqr(*u[j]), *u[j])), r);
-    if (fp2_sgn0(*u[j]) != fp2_sgn0(y)) y = fp2_reduce(fp2_neg(y));
-    *out[j] = iso3_to_jac(x, y);
-  }
+  for (int j = 0; j < 2 && ok; ++j)
+    if (!sswu_map_x1(*u[j], sswu_x1(inv[j]), *out[j])) ok = false;
   if (!ok) {  // exceptional inputs (probability ~2^-380 per hash): reference path
     q0 = map_to_curve_g2(u0);
     q1 = map_to_curve_g2(u1);

@@ -210,50 +210,62 @@ TBG_HD Jac<F> g2_clear_cofactor_g(const Jac<F>& p, bool& exc) {
 // no products by the Montgomery one -- 2 of a line's ~17 products per lane).
 template <class F> struct LineG { F l0, l1, l4; };
 
+// The steps hand each line coefficient to `sink(k, v)` (k = 0, 1, 2 for l0,
+// l1, l4) as soon as it is formed, in an order that retires inputs early:
+// a kernel storing them directly keeps ~6 Fp2 live instead of ~9 (k_lines_h
+// spilled 91 VGPRs with the formula order).  The products are the formulas'
+// own, operand for operand.
+template <class F, bool EVAL = true, class S>
+TBG_HD void miller_dbl_s(Jac<F>& T, const Fp& nxP, const Fp& yP, S&& sink) {
+  const F ZZ = f_sqr(T.Z);
+  const F YZ = f_mul(T.Y, T.Z);
+  const F Z3 = f_reduce(f_add_l(YZ, YZ));
+  const F l4 = f_mul(Z3, ZZ);                              // 2 Y Z^3 yP
+  sink(2, EVAL ? f_mulfp(l4, yP) : l4);
+  const F B = f_sqr(T.Y);
+  const F C = f_sqr(B);
+  const F A = f_sqr(T.X);
+  const F t = f_sub_l(f_sqr(f_add(T.X, B)), f_add(A, C));
+  const F D = f_reduce(f_add_l(t, t));
+  const F E = f_small(A, 3);
+  const F l1 = f_mul(ZZ, E);                               // -3X^2 Z^2 xP
+  sink(1, EVAL ? f_mulfp(l1, nxP) : l1);
+  sink(0, f_reduce(f_sub_l(f_mul(T.X, E), f_add(B, B))));  // 3X^3 - 2Y^2
+  const F X3 = f_reduce(f_sub_l(f_sqr(E), f_add(D, D)));
+  const F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(D, X3), E), f_small(C, 8)));
+  T = {X3, Y3, Z3};
+}
+
+template <class F, bool EVAL = true, class S>
+TBG_HD void miller_add_s(Jac<F>& T, const Aff<F>& Q, const Fp& nxP, const Fp& yP, S&& sink) {
+  const F ZZ = f_sqr(T.Z);
+  const F U2 = f_mul(Q.x, ZZ);
+  const F S2 = f_mul(f_mul(Q.y, T.Z), ZZ);
+  const F H = f_reduce(f_sub_l(U2, T.X));
+  const F R = f_reduce(f_sub_l(S2, T.Y));
+  const F Z3 = f_mul(T.Z, H);
+  sink(2, EVAL ? f_mulfp(Z3, yP) : Z3);
+  sink(1, EVAL ? f_mulfp(R, nxP) : R);
+  sink(0, f_reduce(f_sub_l(f_mul(R, Q.x), f_mul(Q.y, Z3))));
+  const F HH = f_sqr(H);
+  const F HHH = f_mul(H, HH);
+  const F V = f_mul(T.X, HH);
+  const F X3 = f_reduce(f_sub_l(f_sub_l(f_sqr(R), HHH), f_add(V, V)));
+  const F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(V, X3), R), f_mul(T.Y, HHH)));
+  T = {X3, Y3, Z3};
+}
+
 template <class F, bool EVAL = true>
 TBG_HD LineG<F> miller_dbl_g(Jac<F>& T, const Fp& nxP, const Fp& yP) {
-  F A = f_sqr(T.X);
-  F B = f_sqr(T.Y);
-  F C = f_sqr(B);
-  F ZZ = f_sqr(T.Z);
-  F t = f_sub_l(f_sqr(f_add(T.X, B)), f_add(A, C));
-  F D = f_reduce(f_add_l(t, t));
-  F E = f_small(A, 3);
-  F Fv = f_sqr(E);
-  F X3 = f_reduce(f_sub_l(Fv, f_add(D, D)));
-  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(D, X3), E), f_small(C, 8)));
-  F YZ = f_mul(T.Y, T.Z);
-  F Z3 = f_reduce(f_add_l(YZ, YZ));
   LineG<F> l;
-  l.l0 = f_reduce(f_sub_l(f_mul(T.X, E), f_add(B, B)));   // 3X^3 - 2Y^2
-  l.l1 = f_mul(ZZ, E);                                   // -3X^2 Z^2 xP
-  l.l4 = f_mul(Z3, ZZ);                                  // 2 Y Z^3 yP
-  if (EVAL) {
-    l.l1 = f_mulfp(l.l1, nxP);
-    l.l4 = f_mulfp(l.l4, yP);
-  }
-  T = {X3, Y3, Z3};
+  miller_dbl_s<F, EVAL>(T, nxP, yP, [&](int k, const F& v) { (k == 0 ? l.l0 : k == 1 ? l.l1 : l.l4) = v; });
   return l;
 }
 
 template <class F, bool EVAL = true>
 TBG_HD LineG<F> miller_add_g(Jac<F>& T, const Aff<F>& Q, const Fp& nxP, const Fp& yP) {
-  F ZZ = f_sqr(T.Z);
-  F U2 = f_mul(Q.x, ZZ);
-  F S2 = f_mul(f_mul(Q.y, T.Z), ZZ);
-  F H = f_reduce(f_sub_l(U2, T.X));
-  F R = f_reduce(f_sub_l(S2, T.Y));
-  F HH = f_sqr(H);
-  F HHH = f_mul(H, HH);
-  F V = f_mul(T.X, HH);
-  F X3 = f_reduce(f_sub_l(f_sub_l(f_sqr(R), HHH), f_add(V, V)));
-  F Y3 = f_reduce(f_sub_l(f_mul(f_sub_l(V, X3), R), f_mul(T.Y, HHH)));
-  F Z3 = f_mul(T.Z, H);
   LineG<F> l;
-  l.l0 = f_reduce(f_sub_l(f_mul(R, Q.x), f_mul(Q.y, Z3)));
-  l.l1 = EVAL ? f_mulfp(R, nxP) : R;
-  l.l4 = EVAL ? f_mulfp(Z3, yP) : Z3;
-  T = {X3, Y3, Z3};
+  miller_add_s<F, EVAL>(T, Q, nxP, yP, [&](int k, const F& v) { (k == 0 ? l.l0 : k == 1 ? l.l1 : l.l4) = v; });
   return l;
 }
 
@@ -362,13 +374,23 @@ TBG_DEV void px_line_store(uint32_t* dst, const LineG<Fp2x>& l) {
 
 // All 68 lines of Q in loop order (g2_lines_t), Fp2 split over the pair;
 // EVAL = false: P left out (nxP, yP unused).
+// (each coefficient stored as the step forms it)
 template <bool EVAL = true>
 TBG_DEV void px_g2_lines(const Aff<Fp2x>& Q, const Fp& nxP, const Fp& yP, uint32_t* out) {
   Jac<Fp2x> T = jac_from_aff(Q);
-  int idx = 0;
+  const uint32_t par = pair_par();
+  uint32_t* dst = out;
+  auto sink = [&](int k, const Fp2x& v) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) dst[(2 * k + par) * NL + i] = v.v.l[i];
+  };
   for (int i = 62; i >= 0; --i) {
-    px_line_store(out + LINE_WORDS * idx++, miller_dbl_g<Fp2x, EVAL>(T, nxP, yP));
-    if ((X_ABS >> i) & 1) px_line_store(out + LINE_WORDS * idx++, miller_add_g<Fp2x, EVAL>(T, Q, nxP, yP));
+    miller_dbl_s<Fp2x, EVAL>(T, nxP, yP, sink);
+    dst += LINE_WORDS;
+    if ((X_ABS >> i) & 1) {
+      miller_add_s<Fp2x, EVAL>(T, Q, nxP, yP, sink);
+      dst += LINE_WORDS;
+    }
   }
 }
 

@@ -67,29 +67,61 @@ TBG_HD Fp2 fp2_inv(const Fp2& a) {
   return {fp_mul(a.c0, t), fp_mul(fp_neg(a.c1), t)};
 }
 
+// Where the inline square roots keep their input across the exponentiations:
+// in registers (RegKeep), or a kernel's memory slot (k_hash.hip,
+// k_decode.hip: a struct whose put / get store and load with compiler
+// barriers) so that the 28 words are not live across them.
+struct RegKeep {
+  Fp2 v;
+  TBG_HD void put(const Fp2& a) { v = a; }
+  TBG_HD Fp2 get() const { return v; }
+};
+
+#if defined(__HIP__)
+// ... the memory form: the compiler barriers stop the load from reusing the
+// registers of the store
+struct SlotKeep {
+  Fp2* p;
+  __device__ void put(const Fp2& a) const {
+    *p = a;
+    __asm__ __volatile__("" ::: "memory");
+  }
+  __device__ Fp2 get() const {
+    __asm__ __volatile__("" ::: "memory");
+    return *p;
+  }
+};
+#endif
+
 // Square root in Fp2 via two Fp exponentiations (norm method).
 // Returns false when a is not a square.  The root returned is unspecified
-// up to sign; callers fix the sign.
-TBG_NI bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
+// up to sign; callers fix the sign.  _in: inline (window width WIN, a kept
+// by `keep` across the exponentiations); fp2_sqrt: out of line.
+// a in Fp (a1 == 0) takes the first exponentiation only: s = a0^((p+1)/4)
+// has s^2 = a0 chi(a0), so the root is (s, 0) for a residue and (0, s) for a
+// non-residue ((s u)^2 = -s^2 = a0).
+template <int WIN = 3, class Keep = RegKeep>
+TBG_HD bool fp2_sqrt_in(const Fp2& a_in, Fp2& out, Keep keep = Keep{}) {
   Fp2 a = fp2_reduce(a_in);
-  bool a1_zero = fp_is_zero(a.c1);
-  if (a1_zero) {
-    // a in Fp: sqrt(a0) or u * sqrt(-a0)
-    Fp s = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS>(a.c0);
-    if (fp_eq(fp_sqr(s), a.c0)) { out = {s, fp_zero()}; return true; }
-    Fp na = fp_neg(a.c0);
-    Fp s2 = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS>(na);
-    if (fp_eq(fp_sqr(s2), na)) { out = {fp_zero(), s2}; return true; }
-    return false;
+  const bool real = fp_is_zero(a.c1);
+  keep.put(a);
+  const Fp norm = fp_select(real, a.c0, fp_mul2(a.c0, a.c0, a.c1, a.c1));
+  const Fp gamma = fp_pow_const_in<EXP_SQRT_BITS, EXP_SQRT_WORDS, WIN>(norm);
+  a = keep.get();
+  const Fp g2 = fp_sqr(gamma);
+  if (real) {
+    if (fp_eq(g2, a.c0)) out = {gamma, fp_zero()};
+    else if (fp_eq(g2, fp_reduce(fp_neg(a.c0)))) out = {fp_zero(), gamma};
+    else return false;
+    return true;
   }
-  Fp norm = fp_mul2(a.c0, a.c0, a.c1, a.c1);
-  Fp gamma = fp_pow_const<EXP_SQRT_BITS, EXP_SQRT_WORDS>(norm);
-  if (!fp_eq(fp_sqr(gamma), norm)) return false;
-  Fp inv2 = fp_from_const(INV2_M);
-  Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);  // non-zero because a1 != 0
-  Fp t = fp_pow_const<EXP_PM3D4_BITS, EXP_PM3D4_WORDS>(delta);  // delta^((p-3)/4)
-  Fp x0 = fp_mul(delta, t);
-  Fp x0sq = fp_sqr(x0);
+  if (!fp_eq(g2, fp_mul2(a.c0, a.c0, a.c1, a.c1))) return false;
+  const Fp inv2 = fp_from_const(INV2_M);
+  const Fp delta = fp_mul(fp_add(a.c0, gamma), inv2);  // non-zero because a1 != 0
+  const Fp t = fp_pow_const_in<EXP_PM3D4_BITS, EXP_PM3D4_WORDS, WIN>(delta);  // delta^((p-3)/4)
+  a = keep.get();
+  const Fp x0 = fp_mul(delta, t);
+  const Fp x0sq = fp_sqr(x0);
   Fp2 r;
   if (fp_eq(x0sq, delta)) {
     // delta is a residue: x0 = sqrt(delta), x1 = a1 / (2 x0) = a1 t / 2
@@ -104,6 +136,7 @@ TBG_NI bool fp2_sqrt(const Fp2& a_in, Fp2& out) {
   out = r;
   return true;
 }
+TBG_NI bool fp2_sqrt(const Fp2& a_in, Fp2& out) { return fp2_sqrt_in<3>(a_in, out); }
 
 // Legendre-style square test in Fp2: a is a square iff norm(a) is a square in Fp.
 TBG_NI bool fp2_is_square(const Fp2& a) {

@@ -57,16 +57,17 @@ __global__ void TBG_LAUNCH_N(TBG_DECODE_WAVES) k_decode_sigs(DevBatch B) {
   if (i < CNT_WORDS) B.counters[i] = 0;
   if (B.rlc_batch && i <= MSM_BUCKETS) B.msm_off[i] = 0;
   if (i >= B.n_partials) return;
-  uint8_t b[96];
-  for (int j = 0; j < 96; ++j) b[j] = B.sigs[96ull * i + j];
-  G2A a;
-  int32_t st = g2_decompress_t<true, false>(b, a);
+  // decoded from the input bytes straight into the output slot: x and the
+  // root's input wait there while the exponentiations run (the root inline:
+  // the out-of-line form saved its callee-saved registers to scratch on
+  // every call)
+  G2A& a = B.sig_aff[i];
+  int32_t st = g2_decompress_t<true, false>(B.sigs + 96ull * i, a, SlotKeep{&a.y});
   if (st == DEC_IDENTITY) st = TBG_PS_ERR_IDENTITY;
   if (st != DEC_OK) {
     a.x = fp2_zero();
     a.y = fp2_zero();
   }
-  B.sig_aff[i] = a;
   B.partial_status[i] = (st == DEC_OK) ? TBG_PS_NOT_VERIFIED : st;
 }
 

@@ -41,24 +41,40 @@ __device__ __forceinline__ Jac<Fp2x> px_mul_x_full(const Jac<Fp2x>& p) {
   }
   return jac_neg(acc);
 }
+// The rare cases out of line (their registers do not count against the
+// kernels' loop bodies; the complete formulas inline spilled ~360 VGPRs of
+// k_hash_clear_x1 to scratch): [x] p with the complete formulas, and the
+// complete addition.
+__device__ __noinline__ Jac<Fp2x> px_mul_x_complete(const Jac<Fp2x>& p) { return px_mul_x_full(p); }
+__device__ __noinline__ Jac<Fp2x> px_add_complete(const Jac<Fp2x>& a, const Jac<Fp2x>& b) {
+  return jac_add(a, b);  // (its doubling case a call: a branch over an inline doubling is out of range here)
+}
+// a + b, the doubling case (pair-uniform) redone with the complete formulas
+__device__ __forceinline__ Jac<Fp2x> px_add(const Jac<Fp2x>& a, const Jac<Fp2x>& b) {
+  bool exc = false;
+  const Jac<Fp2x> r = jac_add_x(a, b, exc);
+  return pair_all(!exc) ? r : px_add_complete(a, b);
+}
 __device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
 #if TBG_CLEAR_X
   bool exc = false;
   const Jac<Fp2x> acc = jac_mul_xabs_x(p, exc);
   if (pair_all(!exc)) return jac_neg(acc);  // (pair-uniform)
-#endif
+  return px_mul_x_complete(p);
+#else
   return px_mul_x_full(p);
+#endif
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x1(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (m >= B.n_msgs) return;
-  // P = Q0 + Q1, the two SSWU maps' points (k_hash_map)
-  const Jac<Fp2x> p = jac_add_in<Fp2x, true>(px_load(B.h_jac[m]), px_load(B.h_jac[B.n_msgs + m]));
+  // P = Q0 + Q1, the two SSWU maps' points (k_hash_sswu)
+  const Jac<Fp2x> p = px_add(px_load(B.h_jac[m]), px_load(B.h_jac[B.n_msgs + m]));
   px_store(B.h_jac[m], p);
   const Jac<Fp2x> t1 = px_mul_x(p);
   px_store(B.h_jac[B.n_msgs + m], t1);
-  px_store(B.h_jac[2 * B.n_msgs + m], jac_add_in<Fp2x, true>(t1, px_psi(p)));
+  px_store(B.h_jac[2 * B.n_msgs + m], px_add(t1, px_psi(p)));
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x2(DevBatch B) {
@@ -84,14 +100,20 @@ __device__ __noinline__ Jac<Fp2x> clear_fin_complete(const DevBatch& B, uint32_t
 // that skip the doubling case (bls_pair.h jac_add_x) and psi(P) formed where
 // it is used: two live points instead of three (the complete form spilled
 // 654 VGPRs and wrote 4.5 KB of scratch per message)
+// (each operand is loaded where it is used and P read again for the last two
+// terms -- the compiler barriers keep loads from being hoisted across the
+// additions: three live points there spilled ~200 VGPRs)
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_fin(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (m >= B.n_msgs) return;
-  const Jac<Fp2x> p = px_load(B.h_jac[m]);
   bool exc = false;
-  Jac<Fp2x> t3 = px_psi(px_psi(jac_dbl_in(p)));                                 // psi^2(2P)
+  Jac<Fp2x> t3 = px_psi(px_psi(jac_dbl_in(px_load(B.h_jac[m]))));              // psi^2(2P)
+  __asm__ __volatile__("" ::: "memory");
   t3 = jac_add_x(t3, jac_neg(px_load(B.h_jac[B.n_msgs + m])), exc);             // - [x]P
+  __asm__ __volatile__("" ::: "memory");
   t3 = jac_add_x(t3, px_load(B.h_jac[2 * B.n_msgs + m]), exc);                  // + [x]([x]P + psi(P))
+  __asm__ __volatile__("" ::: "memory");
+  const Jac<Fp2x> p = px_load(B.h_jac[m]);
   t3 = jac_add_x(t3, jac_neg(px_psi(p)), exc);                                  // - psi(P)
   t3 = jac_add_x(t3, jac_neg(p), exc);                                          // - P
   if (!pair_all(!exc)) t3 = clear_fin_complete(B, m);  // (pair-uniform)

@@ -161,14 +161,13 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket_part(DevBatch B) {
   px_store(B.msm_part[w], acc);
 }
 
-__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
-  TBG_URGENT();
-  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
-  if (j >= MSM_BUCKETS) return;
-  if (B.counters[CNT_L0_BAD]) return;
+// [2j + 1] (sum of bucket j's slices), with the addition given as F (the
+// kernel's fast form, or the complete formulas of the rare redo)
+template <class Add>
+__device__ __forceinline__ Jac<Fp2x> msm_bucket_scaled(const DevBatch& B, uint32_t j, Add&& add) {
   Jac<Fp2x> acc = px_load(B.msm_part[MSM_SPLIT * j]);
 #pragma unroll 1
-  for (uint32_t sl = 1; sl < MSM_SPLIT; ++sl) acc = jac_add_in<Fp2x, true>(acc, px_load(B.msm_part[MSM_SPLIT * j + sl]));
+  for (uint32_t sl = 1; sl < MSM_SPLIT; ++sl) acc = add(acc, px_load(B.msm_part[MSM_SPLIT * j + sl]));
   const uint32_t m = 2 * j + 1;
   if (m > 1 && !jac_is_inf(acc)) {
     const Jac<Fp2x> b = acc;
@@ -176,9 +175,28 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
 #pragma unroll 1
     for (int bit = top - 1; bit >= 0; --bit) {
       acc = jac_dbl_in(acc);
-      if ((m >> bit) & 1u) acc = jac_add_in<Fp2x, true>(acc, b);
+      if ((m >> bit) & 1u) acc = add(acc, b);
     }
   }
+  return acc;
+}
+// the doubling case of an addition (equal slice sums: crafted signatures
+// only) redone with the complete formulas, out of line
+__device__ __noinline__ Jac<Fp2x> msm_bucket_complete(const DevBatch& B, uint32_t j) {
+  return msm_bucket_scaled(B, j, [](const Jac<Fp2x>& a, const Jac<Fp2x>& b) { return jac_add(a, b); });
+}
+
+// (the additions without the doubling branch: the complete formulas inline
+// spilled 139 VGPRs on this latency-bound tail kernel)
+__global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
+  TBG_URGENT();
+  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
+  if (j >= MSM_BUCKETS) return;
+  if (B.counters[CNT_L0_BAD]) return;
+  bool exc = false;
+  Jac<Fp2x> acc =
+      msm_bucket_scaled(B, j, [&](const Jac<Fp2x>& a, const Jac<Fp2x>& b) { return jac_add_x(a, b, exc); });
+  if (!pair_all(!exc)) acc = msm_bucket_complete(B, j);  // (pair-uniform)
   px_store(B.msm_bkt[j], acc);
 }
 

@@ -889,14 +889,42 @@ int hc_k_subgroup_sigs(const uint8_t* sig96) {
 #endif
   return g2_in_subgroup_aff_in(a) ? 1 : 0;
 }
-// k_hash_map: hash_to_field, both SSWU maps + isogenies, Q0 + Q1
+// k_hash_map: hash_to_field, the SSWU denominators, their inverse (fp2_inv;
+// count_work.py prices the batched form) and each map's x1
+static Fp2 g_hu0, g_hu1, g_hx10, g_hx11;
 void hc_k_hash_map(const uint8_t* msg, uint32_t len) {
-  Fp2 u0, u1;
-  hash_to_field_fp2(msg, len, u0, u1);
-  G2J q0, q1;
-  map_to_curve_g2_pair(u0, u1, q0, q1);
-  (void)q0;
-  (void)q1;
+  hash_to_field_fp2(msg, len, g_hu0, g_hu1);
+  SswuPair w;
+  const Fp2 di = fp2_inv(sswu_pair_den(g_hu0, g_hu1, w));
+  g_hx10 = sswu_x1(fp2_mul(w.den[1], di));
+  g_hx11 = sswu_x1(fp2_mul(w.den[0], di));
+}
+// k_hash_sswu: both maps of the message (two lanes) as the kernel runs them:
+// root at window width SSWU_WIN, x and y, the isogeny
+void hc_k_hash_sswu(void) {
+  const Fp2* u[2] = {&g_hu0, &g_hu1};
+  const Fp2* x1[2] = {&g_hx10, &g_hx11};
+  for (int j = 0; j < 2; ++j) {
+    Fp2 r, x, y;
+    bool sq;
+    if (!fp2_sqrt_or_z_in<SSWU_WIN>(sswu_gx(*x1[j]), r, sq)) continue;
+    sswu_xy(*u[j], *x1[j], r, sq, x, y);
+    (void)iso3_to_jac_in(x, y);
+  }
+}
+// the split map agrees with the reference map (map_to_curve_g2, RFC 9380
+// 6.6.2) on the message's two field elements: 1 when both affine points match
+extern "C" int hc_sswu_split_check(const uint8_t* msg, uint32_t len) {
+  hc_k_hash_map(msg, len);
+  const Fp2* u[2] = {&g_hu0, &g_hu1};
+  const Fp2* x1[2] = {&g_hx10, &g_hx11};
+  for (int j = 0; j < 2; ++j) {
+    G2J q;
+    if (!sswu_map_x1(*u[j], *x1[j], q)) return -1;
+    const G2J ref = map_to_curve_g2(*u[j]);
+    if (!jac_eq(q, ref)) return 0;
+  }
+  return 1;
 }
 // k_hash_clear_x1 / _x2 / _fin on the message's two mapped points
 static G2J g_hq, g_hq0, g_hq1, g_ht1, g_hu;

@@ -460,6 +460,20 @@ def test_word_sha_expand_message_matches_byte_stream():
         assert L.hc_h2f_check(msg, n) == 1, n
 
 
+def test_split_sswu_matches_reference_map():
+    """k_hash.hip's split map (k_hash_map: the denominators' shared inverse
+    and x1; k_hash_sswu: g(x1), the closed-form root at window width SSWU_WIN, x and
+    y, the Horner-form isogeny) gives the same point as the RFC 9380 6.6.2
+    reference map on both field elements of each message."""
+    import ctypes
+    L = lib()
+    L.hc_sswu_split_check.restype = ctypes.c_int
+    L.hc_sswu_split_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+    for n in [0, 1, 5, 32, 33, 64, 77, 96, 200]:
+        msg = bytes((11 * k + 3 * n + 1) & 0xFF for k in range(n))
+        assert L.hc_sswu_split_check(msg, n) == 1, n
+
+
 def test_workgroup_batch_inversion_matches_per_value_inverse():
     """bls_batchinv.h (Montgomery's trick over a workgroup: wave scans, one
     inversion, back-substitution), emulated lane by lane: every present value

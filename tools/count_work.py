@@ -104,7 +104,7 @@ def main():
     # per-kernel probes (one item of each kernel of the level-0 chain)
     for fn in ("hc_k_decode_sigs", "hc_k_subgroup_sigs"):
         getattr(lib, fn).restype = ctypes.c_int
-    for fn in ("hc_k_hash_map", "hc_k_hash_clear_setup", "hc_k_hash_clear_x1", "hc_k_hash_clear_x2",
+    for fn in ("hc_k_hash_map", "hc_k_hash_sswu", "hc_k_hash_clear_setup", "hc_k_hash_clear_x1", "hc_k_hash_clear_x2",
                "hc_k_hash_clear_fin", "hc_k_g2_affine", "hc_k_rlc_g1_l0", "hc_k_msm_entry"):
         getattr(lib, fn).restype = None
     lib.hc_k_rlc_g1_l0.argtypes = [ctypes.c_uint64]
@@ -114,6 +114,7 @@ def main():
     k_subgroup, st = measure(lib.hc_k_subgroup_sigs, sigs[0])
     assert st == 1
     k_hash_map, _ = measure(lib.hc_k_hash_map, msg, len(msg))
+    k_hash_sswu, _ = measure(lib.hc_k_hash_sswu)
     lib.hc_k_hash_clear_setup(msg, len(msg))
     k_clear_x1, _ = measure(lib.hc_k_hash_clear_x1)
     k_clear_x2, _ = measure(lib.hc_k_hash_clear_x2)
@@ -206,6 +207,7 @@ def main():
             "k_sgb_combine": {"per": "partial", "mads": round(sgb_combine)},
             "k_sgb_test": {"per": "partial", "mads": round(sgb_test)},
             "k_hash_map": {"per": "message", "mads": round(k_hash_map)},
+            "k_hash_sswu": {"per": "message", "mads": round(k_hash_sswu)},
             "k_hash_clear_x1": {"per": "message", "mads": round(k_clear_x1)},
             "k_hash_clear_x2": {"per": "message", "mads": round(k_clear_x2)},
             "k_hash_clear_fin": {"per": "message", "mads": round(k_clear_fin)},

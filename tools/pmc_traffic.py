@@ -16,7 +16,7 @@ import sys
 NOT_CHAIN = {"k_sign", "k_sk_to_pk", "k_decode_pubkeys", "k_pubkey_tables"}
 # chain kernels that vector generation also launches (on one batch at a time):
 # only their largest-grid calls belong to the chain
-SHARED = {"k_hash_map", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"}
+SHARED = {"k_hash_map", "k_hash_sswu", "k_hash_clear_x1", "k_hash_clear_x2", "k_hash_clear_fin", "k_hash_affine"}
 
 
 def _grid(r):
