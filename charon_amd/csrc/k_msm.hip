@@ -180,6 +180,9 @@ __device__ __forceinline__ Jac<Fp2x> msm_bucket_scaled(const DevBatch& B, uint32
   }
   return acc;
 }
+#ifndef TBG_MSM_BUCKET_X
+#define TBG_MSM_BUCKET_X 1  // 0: the complete additions inline (139 spilled VGPRs)
+#endif
 // the doubling case of an addition (equal slice sums: crafted signatures
 // only) redone with the complete formulas, out of line
 __device__ __noinline__ Jac<Fp2x> msm_bucket_complete(const DevBatch& B, uint32_t j) {
@@ -193,10 +196,26 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
   const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (j >= MSM_BUCKETS) return;
   if (B.counters[CNT_L0_BAD]) return;
+#if TBG_MSM_BUCKET_X
   bool exc = false;
   Jac<Fp2x> acc =
       msm_bucket_scaled(B, j, [&](const Jac<Fp2x>& a, const Jac<Fp2x>& b) { return jac_add_x(a, b, exc); });
   if (!pair_all(!exc)) acc = msm_bucket_complete(B, j);  // (pair-uniform)
+#else
+  Jac<Fp2x> acc = px_load(B.msm_part[MSM_SPLIT * j]);
+#pragma unroll 1
+  for (uint32_t sl = 1; sl < MSM_SPLIT; ++sl) acc = jac_add_in<Fp2x, true>(acc, px_load(B.msm_part[MSM_SPLIT * j + sl]));
+  const uint32_t m = 2 * j + 1;
+  if (m > 1 && !jac_is_inf(acc)) {
+    const Jac<Fp2x> b = acc;
+    const int top = 31 - __builtin_clz(m);
+#pragma unroll 1
+    for (int bit = top - 1; bit >= 0; --bit) {
+      acc = jac_dbl_in(acc);
+      if ((m >> bit) & 1u) acc = jac_add_in<Fp2x, true>(acc, b);
+    }
+  }
+#endif
   px_store(B.msm_bkt[j], acc);
 }
 
