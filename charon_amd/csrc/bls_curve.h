@@ -304,6 +304,13 @@ enum DecodeStatus : int32_t {
   DEC_ERR_SUBGROUP = -4,
 };
 
+// k_decode_sigs' exponentiation window (the inline root): width 4 spills 71
+// VGPRs and still runs 8.37-8.60 vs 8.73-8.89 ms per 640k signatures at width
+// 3 (profiles/r06/hash/ab_r6q.txt)
+#ifndef TBG_DECODE_WIN
+#define TBG_DECODE_WIN 4
+#endif
+
 // 96-byte ZCash compressed G2 -> affine (Montgomery).  INL = true runs the
 // subgroup check's doublings inline (kernel callers); SUBGROUP = false leaves
 // the subgroup check to the caller (k_decode_sigs hands it to the lane-pair
@@ -331,7 +338,7 @@ TBG_HD int32_t g2_decompress_t(const uint8_t* b, G2A& out, Keep keep = Keep{}) {
   out.x = x;
   const Fp2 rhs = fp2_reduce(fp2_add(fp2_mul(fp2_sqr(x), x), fp2_from_const(B2_M)));
   Fp2 y;
-  if (!(INL ? fp2_sqrt_in<3>(rhs, y, keep) : fp2_sqrt(rhs, y))) return DEC_ERR_NOT_ON_CURVE;
+  if (!(INL ? fp2_sqrt_in<TBG_DECODE_WIN>(rhs, y, keep) : fp2_sqrt(rhs, y))) return DEC_ERR_NOT_ON_CURVE;
   if ((uint32_t)fp2_lex_largest(y) != s_flag) y = fp2_reduce(fp2_neg(y));
   out.y = y;
   if (SUBGROUP && !(INL ? g2_in_subgroup_aff_in(out) : g2_in_subgroup(jac_from_aff(out)))) return DEC_ERR_SUBGROUP;
