@@ -21,23 +21,23 @@
 
 namespace tbg {
 
-// 64 bits of SHA-256's compression function keyed by the 32-byte batch seed.
+// 64 bits of SHA-256's compression function keyed by the 32-byte batch seed:
+// one block seed || i || 0x80 || 0... built as words in registers (the
+// byte-stream sha256_block kept the block and its schedule in scratch).
+TBG_HD void rlc_block(const uint32_t (&seed)[8], uint32_t i, uint32_t tag, uint32_t (&h)[8]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = seed[k];
+  w[8] = i;
+  w[9] = tag;
+#pragma unroll
+  for (int k = 10; k < 16; ++k) w[k] = 0;
+  sha256_iv(h);
+  sha256_compress(h, w);
+}
 TBG_HD uint64_t rlc_scalar(const uint32_t (&seed)[8], uint32_t i) {
-  uint8_t blk[64];
-  for (int k = 0; k < 8; ++k) {
-    blk[4 * k] = (uint8_t)(seed[k] >> 24);
-    blk[4 * k + 1] = (uint8_t)(seed[k] >> 16);
-    blk[4 * k + 2] = (uint8_t)(seed[k] >> 8);
-    blk[4 * k + 3] = (uint8_t)seed[k];
-  }
-  for (int k = 32; k < 64; ++k) blk[k] = 0;
-  blk[32] = (uint8_t)(i >> 24);
-  blk[33] = (uint8_t)(i >> 16);
-  blk[34] = (uint8_t)(i >> 8);
-  blk[35] = (uint8_t)i;
-  blk[36] = 0x80;
-  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au, 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-  sha256_block(h, blk);
+  uint32_t h[8];
+  rlc_block(seed, i, 0x80000000u, h);
   uint64_t r = ((uint64_t)h[0] << 32) | h[1];
   return r ? r : 1;
 }
@@ -46,6 +46,10 @@ TBG_HD uint64_t rlc_scalar(const uint32_t (&seed)[8], uint32_t i) {
 // signed digits c_k in [-6, 6] -- uniform mod 13 -- from the same keyed
 // compression function on a separate message (a tag byte after i), four
 // base-13 digits per 32-bit word (13^4 = 28561: bias < 2^-17 per digit).
+// (The byte-stream sha256_block call here, not rlc_block's unrolled register
+// form: that took k_sgb_sort from 66 to 256 VGPRs -- one wave per SIMD for
+// its four-wave workgroups, which then waited for four free SIMDs on a CU
+// behind the other launches' kernels: -1.3 % on the driver shape.)
 TBG_HD void sgb_digits(const uint32_t (&seed)[8], uint32_t i, int32_t (&c)[18]) {
   uint8_t blk[64];
   for (int k = 0; k < 8; ++k) {

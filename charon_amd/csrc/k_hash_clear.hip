@@ -49,39 +49,60 @@ __device__ __noinline__ Jac<Fp2x> px_mul_x_complete(const Jac<Fp2x>& p) { return
 __device__ __noinline__ Jac<Fp2x> px_add_complete(const Jac<Fp2x>& a, const Jac<Fp2x>& b) {
   return jac_add(a, b);  // (its doubling case a call: a branch over an inline doubling is out of range here)
 }
-// a + b, the doubling case (pair-uniform) redone with the complete formulas
-__device__ __forceinline__ Jac<Fp2x> px_add(const Jac<Fp2x>& a, const Jac<Fp2x>& b) {
-  bool exc = false;
-  const Jac<Fp2x> r = jac_add_x(a, b, exc);
-  return pair_all(!exc) ? r : px_add_complete(a, b);
+// a + b (b: psi(b) when PSI) from their slots, with the complete formulas
+__device__ __forceinline__ Jac<Fp2x> px_psi(const Jac<Fp2x>& p);
+__device__ __noinline__ Jac<Fp2x> px_add_complete_at(const G2J* a, const G2J* b, bool psi) {
+  const Jac<Fp2x> q = px_load(*b);
+  return px_add_complete(px_load(*a), psi ? px_psi(q) : q);
 }
-__device__ __forceinline__ Jac<Fp2x> px_mul_x(const Jac<Fp2x>& p) {
+// [x] p for p in its h_jac slot, re-read at each of the five additions
+// (the compiler barrier keeps the load where it is used: a base point held
+// across the 63 doublings was spilled to scratch and reloaded every step)
+__device__ __forceinline__ Jac<Fp2x> px_mul_x(const G2J& slot) {
 #if TBG_CLEAR_X
   bool exc = false;
-  const Jac<Fp2x> acc = jac_mul_xabs_x(p, exc);
+  Jac<Fp2x> acc = px_load(slot);
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    acc = jac_dbl_lo(acc);
+    if ((X_ABS >> i) & 1) {
+      __asm__ __volatile__("" ::: "memory");
+      acc = jac_add_x(acc, px_load(slot), exc);
+    }
+  }
   if (pair_all(!exc)) return jac_neg(acc);  // (pair-uniform)
-  return px_mul_x_complete(p);
+  return px_mul_x_complete(px_load(slot));
 #else
-  return px_mul_x_full(p);
+  return px_mul_x_full(px_load(slot));
 #endif
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x1(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;  // both lanes of a pair take the same branches
   if (m >= B.n_msgs) return;
-  // P = Q0 + Q1, the two SSWU maps' points (k_hash_sswu)
-  const Jac<Fp2x> p = px_add(px_load(B.h_jac[m]), px_load(B.h_jac[B.n_msgs + m]));
-  px_store(B.h_jac[m], p);
-  const Jac<Fp2x> t1 = px_mul_x(p);
-  px_store(B.h_jac[B.n_msgs + m], t1);
-  px_store(B.h_jac[2 * B.n_msgs + m], px_add(t1, px_psi(p)));
+  G2J* h = B.h_jac + m;
+  const uint32_t n = B.n_msgs;
+  // P = Q0 + Q1, the two SSWU maps' points (k_hash_sswu); the rare doubling
+  // case redone from the slots (nothing held in registers for it)
+  bool exc = false;
+  Jac<Fp2x> p = jac_add_x(px_load(h[0]), px_load(h[n]), exc);
+  if (!pair_all(!exc)) p = px_add_complete_at(h, h + n, false);  // (pair-uniform)
+  px_store(h[0], p);
+  __asm__ __volatile__("" ::: "memory");
+  const Jac<Fp2x> t1 = px_mul_x(h[0]);
+  px_store(h[n], t1);
+  __asm__ __volatile__("" ::: "memory");
+  exc = false;
+  Jac<Fp2x> u = jac_add_x(t1, px_psi(px_load(h[0])), exc);
+  if (!pair_all(!exc)) u = px_add_complete_at(h + n, h, true);
+  px_store(h[2 * n], u);
 }
 
 __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_hash_clear_x2(DevBatch B) {
   const uint32_t m = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (m >= B.n_msgs) return;
   G2J* u = B.h_jac + 2 * B.n_msgs + m;
-  px_store(*u, px_mul_x(px_load(*u)));
+  px_store(*u, px_mul_x(*u));
 }
 
 // The combination with the complete additions (out-of-line calls): the rare

@@ -161,21 +161,31 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket_part(DevBatch B) {
   px_store(B.msm_part[w], acc);
 }
 
-// [2j + 1] (sum of bucket j's slices), with the addition given as F (the
-// kernel's fast form, or the complete formulas of the rare redo)
-template <class Add>
-__device__ __forceinline__ Jac<Fp2x> msm_bucket_scaled(const DevBatch& B, uint32_t j, Add&& add) {
+// [2j + 1] (sum of bucket j's slices): FAST = the additions without the
+// doubling branch (`exc` set when one needed it), else the complete formulas
+// (out-of-line calls)
+template <bool FAST>
+__device__ __forceinline__ Jac<Fp2x> msm_bucket_scaled(const DevBatch& B, uint32_t j, bool& exc) {
   Jac<Fp2x> acc = px_load(B.msm_part[MSM_SPLIT * j]);
 #pragma unroll 1
-  for (uint32_t sl = 1; sl < MSM_SPLIT; ++sl) acc = add(acc, px_load(B.msm_part[MSM_SPLIT * j + sl]));
+  for (uint32_t sl = 1; sl < MSM_SPLIT; ++sl) {
+    const Jac<Fp2x> q = px_load(B.msm_part[MSM_SPLIT * j + sl]);
+    acc = FAST ? jac_add_x(acc, q, exc) : jac_add(acc, q);
+  }
   const uint32_t m = 2 * j + 1;
   if (m > 1 && !jac_is_inf(acc)) {
-    const Jac<Fp2x> b = acc;
+    // the base waits in the output slot, read where it is added (held in
+    // registers across the ladder it spilled ~40 words per step)
+    px_store(B.msm_bkt[j], acc);
     const int top = 31 - __builtin_clz(m);
 #pragma unroll 1
     for (int bit = top - 1; bit >= 0; --bit) {
       acc = jac_dbl_in(acc);
-      if ((m >> bit) & 1u) acc = add(acc, b);
+      if ((m >> bit) & 1u) {
+        __asm__ __volatile__("" ::: "memory");
+        const Jac<Fp2x> b = px_load(B.msm_bkt[j]);
+        acc = FAST ? jac_add_x(acc, b, exc) : jac_add(acc, b);
+      }
     }
   }
   return acc;
@@ -186,7 +196,8 @@ __device__ __forceinline__ Jac<Fp2x> msm_bucket_scaled(const DevBatch& B, uint32
 // the doubling case of an addition (equal slice sums: crafted signatures
 // only) redone with the complete formulas, out of line
 __device__ __noinline__ Jac<Fp2x> msm_bucket_complete(const DevBatch& B, uint32_t j) {
-  return msm_bucket_scaled(B, j, [](const Jac<Fp2x>& a, const Jac<Fp2x>& b) { return jac_add(a, b); });
+  bool unused = false;
+  return msm_bucket_scaled<false>(B, j, unused);
 }
 
 // (the additions without the doubling branch: the complete formulas inline
@@ -198,8 +209,7 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_msm_bucket(DevBatch B) {
   if (B.counters[CNT_L0_BAD]) return;
 #if TBG_MSM_BUCKET_X
   bool exc = false;
-  Jac<Fp2x> acc =
-      msm_bucket_scaled(B, j, [&](const Jac<Fp2x>& a, const Jac<Fp2x>& b) { return jac_add_x(a, b, exc); });
+  Jac<Fp2x> acc = msm_bucket_scaled<true>(B, j, exc);
   if (!pair_all(!exc)) acc = msm_bucket_complete(B, j);  // (pair-uniform)
 #else
   Jac<Fp2x> acc = px_load(B.msm_part[MSM_SPLIT * j]);

@@ -34,7 +34,10 @@
 
 namespace tbg {
 
-constexpr uint32_t kSgbSortBlock = 256;
+#ifndef TBG_SGB_SORT_BLOCK
+#define TBG_SGB_SORT_BLOCK 256
+#endif
+constexpr uint32_t kSgbSortBlock = TBG_SGB_SORT_BLOCK;  // threads per group's sort
 
 __global__ void __launch_bounds__(kSgbSortBlock) k_sgb_sort(DevBatch B) {
   __shared__ uint32_t cnt[SGB_BUCKETS];
@@ -154,15 +157,26 @@ __global__ void TBG_LAUNCH_N(TBG_PAIR_WAVES) k_sgb_test(DevBatch B, uint32_t n_s
   const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 1;
   if (w >= n_sg * SGB_K) return;
   const uint32_t g = w / SGB_K, k = w % SGB_K;
-  const Jac<Fp2x> q = px_load(B.sgb_part[((size_t)SGB_BUCKETS * g + (size_t)SGB_V * k) * B.sgb_split]);
+  const G2J& slot = B.sgb_part[((size_t)SGB_BUCKETS * g + (size_t)SGB_V * k) * B.sgb_split];
   bool ok = true;
-  if (!jac_is_inf(q)) {
+  if (!jac_is_inf(px_load(slot))) {
+    // [|x|] Q with Q re-read from its slot where it is added (held across the
+    // doublings it went through scratch every step)
     bool exc = false;
-    const Jac<Fp2x> m = jac_mul_xabs_x(q, exc);  // [|x|] Q; psi(Q) == [x] Q == -m
+    Jac<Fp2x> m = px_load(slot);
+#pragma unroll 1
+    for (int i = 62; i >= 0; --i) {
+      m = jac_dbl_lo(m);
+      if ((X_ABS >> i) & 1) {
+        __asm__ __volatile__("" ::: "memory");
+        m = jac_add_x(m, px_load(slot), exc);
+      }
+    }  // psi(Q) == [x] Q == -m
     if (exc || jac_is_inf(m)) {
       ok = false;
     } else {
-      const Jac<Fp2x> ps = g2_psi_g(q);
+      __asm__ __volatile__("" ::: "memory");
+      const Jac<Fp2x> ps = g2_psi_g(px_load(slot));
       const Fp2x z1 = f_sqr(ps.Z), z2 = f_sqr(m.Z);
       ok = f_eq(f_mul(ps.X, z2), f_mul(m.X, z1)) &&
            f_eq(f_mul(f_mul(ps.Y, m.Z), z2), f_reduce(f_neg(f_mul(f_mul(m.Y, ps.Z), z1))));
