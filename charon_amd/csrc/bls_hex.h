@@ -184,7 +184,7 @@ namespace tbg {
 // round 4: profiles/r04/lazy/; removed.)
 // Fp12 slot of global thread t (UINT32_MAX for lane 15 of a row), and the
 // threads n slots need: 10 per wave.
-TBG_HD inline uint32_t hex_slot(uint32_t t) {
+TBG_HD uint32_t hex_slot(uint32_t t) {
   const uint32_t l = t & 15u;
   return l == 15u ? 0xFFFFFFFFu : (t >> 6) * 10u + ((t >> 5) & 1u) * 5u + l / 3u;
 }

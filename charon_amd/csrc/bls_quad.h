@@ -157,7 +157,7 @@ constexpr int DPP_SHL1 = 0x101, DPP_SHL2 = 0x102, DPP_SHR1 = 0x111, DPP_SHR2 = 0
 TBG_DEV int quad_lane() { return (int)((threadIdx.x & 15u) % 3u); }
 // Fp12 slot of global thread t (UINT32_MAX for the idle lane 15 of a row),
 // and the threads n slots need.
-TBG_HD inline uint32_t fp12_slot(uint32_t t) {
+TBG_HD uint32_t fp12_slot(uint32_t t) {
   const uint32_t l = t & 15u;
   return l == 15u ? 0xFFFFFFFFu : (t >> 4) * 5u + l / 3u;
 }

@@ -491,14 +491,18 @@ static int launch_chain(tbg_ctx* c, const Slot& sl, const DevBatch& B, hipEvent_
     HIP_TRY(hipEventRecord(ev[2], st));
     return TBG_OK;
   };
+  // TBG_ALT_ORDER: on one stream, odd slots run the per-signature chain
+  // first, so launches in flight together are out of phase (one launch's
+  // latency-bound subgroup / MSM tails beside another's hash).
+  const bool alt = TBG_ALT_ORDER && st == st2 && ((&sl - c->slots.data()) & 1);
   int rc;
   if (stage < 0 || stage == 0) {
     HIP_TRY(hipEventRecord(ev[0], st));
     HIP_TRY(hipStreamWaitEvent(st2, ev[0], 0));
-    if ((rc = msg_chain()) != TBG_OK) return rc;
+    if ((rc = alt ? sig_chain() : msg_chain()) != TBG_OK) return rc;
   }
   if (stage < 0 || stage == 1)
-    if ((rc = sig_chain()) != TBG_OK) return rc;
+    if ((rc = alt ? msg_chain() : sig_chain()) != TBG_OK) return rc;
   if (stage >= 0 && stage != 2) return TBG_OK;
   HIP_TRY(hipStreamWaitEvent(st, ev[5], 0));
   HIP_TRY(hipEventRecord(ev[6], st));
