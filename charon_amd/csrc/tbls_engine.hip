@@ -1216,9 +1216,22 @@ int tbg_replay_plan(tbg_ctx* c, const tbg_ticket* tickets, const uint32_t* n_par
         }
     }
 #endif
-    for (int stage = 0; stage < 3 && rc == TBG_OK; ++stage)
+    for (int stage = 0; stage < 3 && rc == TBG_OK; ++stage) {
+#if TBG_L0_JOIN
+      // The run's level-0 Miller kernels start once every launch of the run
+      // has its signature side (S, P_d, S's lines): a Miller kernel that
+      // starts early holds the SIMDs for ~14 ms while the other launches'
+      // one-workgroup MSM tails wait for a slot behind it.
+      if (stage == 2 && k1 - k0 > 1)
+        for (uint32_t k = k0; k < k1 && rc == TBG_OK; ++k)
+          for (uint32_t j = k0; j < k1; ++j)
+            if (j != k && bs[k].rlc_batch && bs[j].rlc_batch &&
+                hipStreamWaitEvent(sl[k]->st, ev[(size_t)kChainEvents * j + 2], 0) != hipSuccess)
+              rc = TBG_E_DEVICE;
+#endif
       for (uint32_t k = k0; k < k1 && rc == TBG_OK; ++k)
         rc = launch_chain(c, *sl[k], bs[k], ev.data() + (size_t)kChainEvents * k, stage);
+    }
     for (uint32_t k = k0; k < k1; ++k) sl[k]->last = bs[k];
     k0 = k1;
   }

@@ -300,6 +300,9 @@ TBG_HD void fb_pass_loop(const DevBatch& B, uint32_t first, uint32_t stride, uin
 #ifndef TBG_ALT_ORDER
 #define TBG_ALT_ORDER 0
 #endif
+#ifndef TBG_L0_JOIN
+#define TBG_L0_JOIN 0
+#endif
 // Participation of a partial in its duty's aggregate.  SPEC: the
 // speculative aggregation that runs BEFORE verification while level 0 is on
 // (launch_chain): every candidate counts as valid, which is what a level-0
