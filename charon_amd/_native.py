@@ -48,11 +48,22 @@ def is_stale():
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(s) > t for s in sources())
+    # (this file holds the compile flags)
+    return any(os.path.getmtime(s) > t for s in list(sources()) + [os.path.abspath(__file__)])
+
+
+# Per-translation-unit compiler flags on top of the common ones.  The
+# machine scheduler's max-ILP strategy for the decode and Miller units
+# (k_decode_sigs -3 %, k_miller_hex<L0> -2 % with unchanged occupancy;
+# driver shape +1.6 %, profiles/r06/ilp/).  Library-wide it raised small
+# kernels' VGPRs (k_sgb_sort 66 -> 119: 7 -> 4 waves) and the SSWU spills,
+# and lost at 20 steps although every big kernel ran faster alone.
+_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+UNIT_FLAGS: dict = {"k_decode.hip": _ILP, "k_miller_hex.hip": _ILP}
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(), out: str | None = None,
-          extra_flags=(), link_flags=()) -> str:
+          extra_flags=(), link_flags=(), unit_flags=None) -> str:
     """Compile the engine for gfx950: every csrc/*.hip translation unit in
     parallel (hipcc -c), then link libtbls_gpu.so.  `defines` / `out` build a
     tuning variant elsewhere (tools/ab_variants.py)."""
@@ -73,9 +84,11 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-pass-failed", "-Wno-unused-result", "-Wno-unused-value"]
     flags += ["-D" + d for d in defines] + list(extra_flags)
 
+    unit_flags = UNIT_FLAGS if unit_flags is None else unit_flags
+    stamp_text = " ".join(flags) + "".join(f" [{u}: {' '.join(f)}]" for u, f in sorted(unit_flags.items()))
     headers = [s for s in sources() if s.endswith(".h")]
     stamp = os.path.join(objdir, "flags.txt")
-    same_flags = os.path.exists(stamp) and open(stamp).read() == " ".join(flags)
+    same_flags = os.path.exists(stamp) and open(stamp).read() == stamp_text
 
     host_flags = ["-O3", "-std=c++17", "-fPIC"] + ["-D" + d for d in defines] + \
         [f for f in extra_flags if f != "-Xarch_host"]
@@ -92,7 +105,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
         if u.endswith(".cpp"):
             cmd = [_clangxx()] + host_flags + ["-c", os.path.join(CSRC, u), "-o", obj]
         else:
-            cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, u), "-o", obj]
+            cmd = [hipcc] + flags + list(unit_flags.get(u, ())) + ["-c", os.path.join(CSRC, u), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
@@ -104,7 +117,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(),
     for obj in objs:
         check_return_address(obj)
     with open(stamp, "w") as f:
-        f.write(" ".join(flags))
+        f.write(stamp_text)
     cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC"] + list(link_flags) + objs + ["-o", target + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
