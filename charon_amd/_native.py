@@ -55,11 +55,13 @@ def is_stale():
 # Per-translation-unit compiler flags on top of the common ones.  The
 # machine scheduler's max-ILP strategy for the decode and Miller units
 # (k_decode_sigs -3 %, k_miller_hex<L0> -2 % with unchanged occupancy;
-# driver shape +1.6 %, profiles/r06/ilp/).  Library-wide it raised small
+# driver shape +1.6 %, profiles/r06/ilp/), then also the H(m)-lines,
+# cofactor and aggregation units (+0.75 %, ilp/units_more/).  Library-wide it raised small
 # kernels' VGPRs (k_sgb_sort 66 -> 119: 7 -> 4 waves) and the SSWU spills,
 # and lost at 20 steps although every big kernel ran faster alone.
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-UNIT_FLAGS: dict = {"k_decode.hip": _ILP, "k_miller_hex.hip": _ILP}
+UNIT_FLAGS: dict = {u: _ILP for u in ("k_decode.hip", "k_miller_hex.hip", "k_verify.hip", "k_hash_clear.hip",
+                                       "k_aggregate.hip")}
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(), out: str | None = None,
